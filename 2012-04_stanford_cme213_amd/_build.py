@@ -1,0 +1,145 @@
+"""Native build for cme213x: hipcc (gfx950) + g++/OpenMP, in-tree outputs.
+
+Produces two shared libraries under ``<package>/lib``:
+
+* ``libcme213_hip.so`` -- every HIP kernel + launcher (``csrc/hip/*.hip``),
+  cross-compiled for gfx950 with hipcc. Built without a GPU.
+* ``libcme213_cpu.so`` -- OpenMP CPU backends / oracles (``csrc/cpu/*.cpp``),
+  g++ -O3 -fopenmp -ffp-contract=off.
+
+Replaces the reference's per-assignment Makefiles (``hw/*/programming/Makefile``:
+``nvcc -O3 -arch=sm_20``; ``DEBUG=1`` -> ``-g``) with one incremental builder.
+``CME_DEBUG=1`` builds with ``-O1 -g`` (the reference's ``make DEBUG=1``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+INCLUDE = CSRC / "include"
+LIB_DIR = PKG_DIR / "lib"
+OBJ_DIR = REPO / "build" / "obj"
+
+ARCH = os.environ.get("CME_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", shutil.which("g++") or "g++")
+
+HIP_LIB = LIB_DIR / "libcme213_hip.so"
+CPU_LIB = LIB_DIR / "libcme213_cpu.so"
+
+
+def _debug() -> bool:
+    return os.environ.get("CME_DEBUG", "0") not in ("", "0")
+
+
+def _hip_flags() -> list[str]:
+    opt = ["-O1", "-g"] if _debug() else ["-O3"]
+    return opt + [
+        f"--offload-arch={ARCH}",
+        "-std=c++17",
+        "-fPIC",
+        "-munsafe-fp-atomics",
+        "-Wall",
+        "-Wno-unused-function",
+        "-Wno-unused-variable",
+        "-Wno-unknown-pragmas",
+        f"-I{INCLUDE}",
+    ]
+
+
+def _cpu_flags() -> list[str]:
+    opt = ["-O1", "-g"] if _debug() else ["-O3"]
+    return opt + [
+        "-std=c++17",
+        "-fPIC",
+        "-fopenmp",
+        "-ffp-contract=off",
+        "-Wall",
+        "-Wno-unknown-pragmas",
+        "-Wno-unused-function",
+        f"-I{INCLUDE}",
+    ]
+
+
+def _newest_header() -> float:
+    return max((p.stat().st_mtime for p in INCLUDE.rglob("*.h")), default=0.0)
+
+
+def _needs(obj: Path, src: Path, hdr_time: float) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or hdr_time > t
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{proc.stdout}\n{proc.stderr}")
+
+
+def _compile_all(srcs: list[Path], kind: str, jobs: int, verbose: bool) -> list[Path]:
+    hdr = _newest_header()
+    out_dir = OBJ_DIR / kind
+    out_dir.mkdir(parents=True, exist_ok=True)
+    tasks = []
+    objs = []
+    for s in srcs:
+        o = out_dir / (s.stem + ".o")
+        objs.append(o)
+        if _needs(o, s, hdr):
+            if kind == "hip":
+                cmd = [HIPCC, *_hip_flags(), "-c", str(s), "-o", str(o)]
+            else:
+                cmd = [CXX, *_cpu_flags(), "-c", str(s), "-o", str(o)]
+            tasks.append(cmd)
+    if tasks:
+        if verbose:
+            print(f"[cme213x build] compiling {len(tasks)} {kind} source(s)", file=sys.stderr)
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            for f in [ex.submit(_run, c) for c in tasks]:
+                f.result()
+    return objs
+
+
+def _link(objs: list[Path], out: Path, kind: str) -> None:
+    if out.exists() and all(o.stat().st_mtime <= out.stat().st_mtime for o in objs):
+        return
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_suffix(".so.tmp")
+    if kind == "hip":
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    else:
+        cmd = [CXX, "-shared", "-fPIC", "-fopenmp", "-o", str(tmp), *map(str, objs)]
+    _run(cmd)
+    os.replace(tmp, out)
+
+
+def build(jobs: int | None = None, verbose: bool = True, hip: bool = True, cpu: bool = True) -> dict:
+    """Compile every native source; returns {'hip': path|None, 'cpu': path|None}."""
+    jobs = jobs or min(16, os.cpu_count() or 4)
+    out: dict = {"hip": None, "cpu": None}
+    if cpu:
+        srcs = sorted((CSRC / "cpu").glob("*.cpp"))
+        objs = _compile_all(srcs, "cpu", jobs, verbose)
+        _link(objs, CPU_LIB, "cpu")
+        out["cpu"] = CPU_LIB
+    if hip:
+        srcs = sorted((CSRC / "hip").glob("*.hip"))
+        objs = _compile_all(srcs, "hip", jobs, verbose)
+        _link(objs, HIP_LIB, "hip")
+        out["hip"] = HIP_LIB
+    return out
+
+
+if __name__ == "__main__":
+    res = build()
+    for k, v in res.items():
+        print(f"{k}: {v}")

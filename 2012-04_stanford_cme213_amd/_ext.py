@@ -1,0 +1,128 @@
+"""Loader for the in-tree native libraries (ctypes, C ABI).
+
+``libcme213_hip.so`` holds every HIP kernel; ``libcme213_cpu.so`` the OpenMP
+backends. Both are built in-tree by :mod:`._build` (``__graft_entry__.build``).
+
+Policy (no silent fallbacks): when a GPU is visible the HIP library MUST load --
+any op called on a ``cuda`` tensor raises if it cannot. CPU ops always use the
+native OpenMP library; pure-PyTorch code is only ever used as a test oracle.
+
+Every native entry point returns an ``int`` status (``hipError_t`` for HIP
+launchers, 0/1 for CPU), checked by :func:`check` -- the replacement for the
+reference's ``check_launch`` (``hw/hw1/programming/mp1-util.h:8-18``), minus the
+device synchronisation and ``exit(1)``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_LIB_DIR = Path(__file__).resolve().parent / "lib"
+_lock = threading.Lock()
+_libs: dict[str, ctypes.CDLL] = {}
+
+_CT = {
+    "p": ctypes.c_void_p,
+    "i": ctypes.c_int,
+    "u": ctypes.c_uint,
+    "q": ctypes.c_int64,
+    "Q": ctypes.c_uint64,
+    "f": ctypes.c_float,
+    "d": ctypes.c_double,
+    "s": ctypes.c_char_p,
+}
+
+# name -> argument signature (return type is always int)
+HIP_PROTOS: dict[str, str] = {}
+CPU_PROTOS: dict[str, str] = {}
+
+
+def proto(table: dict, name: str, sig: str) -> None:
+    table[name] = sig
+
+
+_bound: dict[tuple[str, str], object] = {}
+
+
+def _fn(kind: str, name: str):
+    """Bound native function (argtypes from the proto table, lazily)."""
+    key = (kind, name)
+    f = _bound.get(key)
+    if f is None:
+        lib = _load(kind)
+        protos = HIP_PROTOS if kind == "hip" else CPU_PROTOS
+        if name not in protos:
+            raise KeyError(f"no prototype registered for {kind}:{name}")
+        f = getattr(lib, name)
+        f.restype = ctypes.c_int
+        f.argtypes = [_CT[c] for c in protos[name].replace(" ", "")]
+        _bound[key] = f
+    return f
+
+
+def _load(kind: str) -> ctypes.CDLL:
+    with _lock:
+        if kind in _libs:
+            return _libs[kind]
+        path = _LIB_DIR / f"libcme213_{kind}.so"
+        if not path.exists():
+            if os.environ.get("CME_AUTOBUILD", "1") != "0":
+                from . import _build
+
+                _build.build(hip=(kind == "hip"), cpu=(kind == "cpu"), verbose=True)
+            if not path.exists():
+                raise RuntimeError(f"cme213x native library missing: {path} (run __graft_entry__.build())")
+        # torch is imported first so its bundled libamdhip64.so.7 (same SONAME)
+        # is the one our HIP library binds to: one HIP runtime per process.
+        lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        if kind == "hip":
+            lib.cme_hip_error_string.restype = ctypes.c_char_p
+            lib.cme_hip_error_string.argtypes = [ctypes.c_int]
+        _libs[kind] = lib
+        return lib
+
+
+def hip() -> ctypes.CDLL:
+    return _load("hip")
+
+
+def cpu() -> ctypes.CDLL:
+    return _load("cpu")
+
+
+def hip_loaded() -> bool:
+    return "hip" in _libs
+
+
+def check(rc: int, what: str, kind: str = "hip") -> None:
+    if rc != 0:
+        if kind == "hip":
+            msg = hip().cme_hip_error_string(int(rc)).decode()
+            raise RuntimeError(f"{what}: HIP error {rc} ({msg})")
+        raise RuntimeError(f"{what}: native CPU backend returned {rc}")
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    """hipStream_t of torch's current stream (so launches order with torch ops
+    and are captured by torch.cuda.CUDAGraph / hipGraph)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def call_hip(name: str, *args) -> None:
+    check(_fn("hip", name)(*args), name, "hip")
+
+
+def call_cpu(name: str, *args) -> None:
+    check(_fn("cpu", name)(*args), name, "cpu")
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()

@@ -1,0 +1,90 @@
+"""2-D heat-stencil op: one FTCS sweep over a region of a pitched grid.
+
+Tensors are 2-D ``(rows, pitch)`` views, contiguous, ``pitch % 64 == 0``;
+``cuda`` tensors run the HIP kernels (``csrc/hip/heat2d.hip``), ``cpu`` tensors
+the OpenMP oracle (``csrc/cpu/heat2d_cpu.cpp``). Parity target: the reference's
+``gpuComputation`` / ``gpuComputationShared*`` and ``cpuComputation``
+(``hw/hw2/solution/2dHeat_solution.cu:371-669``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiip")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f64", "ppiiiiiiddi")
+
+VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3}
+
+
+def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
+    if prev.dim() != 2 or curr.shape != prev.shape:
+        raise ValueError("prev/curr must be equal-shape 2-D (rows, pitch) tensors")
+    if prev.dtype != curr.dtype or prev.device != curr.device:
+        raise ValueError("prev/curr dtype/device mismatch")
+    if prev.dtype not in (torch.float32, torch.float64):
+        raise TypeError("heat stencil supports float32/float64")
+    if not (prev.is_contiguous() and curr.is_contiguous()):
+        raise ValueError("prev/curr must be contiguous")
+    if prev.shape[1] % 64:
+        raise ValueError("pitch (row length) must be a multiple of 64 elements")
+
+
+def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, int, int], order: int,
+              xcfl: float, ycfl: float, variant: str = "stream", chunk: int = 0) -> None:
+    """curr[region] = FTCS(prev); region = (xb, xe, yb, ye) in grid coords."""
+    _check(prev, curr)
+    xb, xe, yb, ye = map(int, region)
+    rows, pitch = prev.shape
+    f64 = prev.dtype == torch.float64
+    if prev.is_cuda:
+        name = "cme_heat_step_f64" if f64 else "cme_heat_step_f32"
+        _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, xb, xe, yb, ye, order,
+                      VARIANTS[variant], xcfl, ycfl, chunk, _ext.stream_ptr(prev.device))
+    else:
+        name = "cme_cpu_heat_step_f64" if f64 else "cme_cpu_heat_step_f32"
+        _ext.call_cpu(name, prev.data_ptr(), curr.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl)
+
+
+def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
+             ycfl: float, iters: int, variant: str = "stream", chunk: int = 0) -> torch.Tensor:
+    """``iters`` ping-pong sweeps starting from ``a``; returns the buffer holding
+    the final state (``a`` if iters is even, else ``b``)."""
+    _check(a, b)
+    xb, xe, yb, ye = map(int, region)
+    rows, pitch = a.shape
+    f64 = a.dtype == torch.float64
+    if a.is_cuda:
+        name = "cme_heat_run_f64" if f64 else "cme_heat_run_f32"
+        _ext.call_hip(name, a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, VARIANTS[variant],
+                      xcfl, ycfl, iters, chunk, _ext.stream_ptr(a.device))
+    else:
+        name = "cme_cpu_heat_run_f64" if f64 else "cme_cpu_heat_run_f32"
+        _ext.call_cpu(name, a.data_ptr(), b.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl, iters)
+    return a if iters % 2 == 0 else b
+
+
+def heat_step_torch(prev: torch.Tensor, region, order: int, xcfl: float, ycfl: float) -> torch.Tensor:
+    """Plain-PyTorch fp oracle of one sweep (returns a new tensor). Used only by
+    tests to cross-check the native CPU oracle itself."""
+    coeffs = {2: [1.0, -2.0, 1.0], 4: [-1.0, 16.0, -30.0, 16.0, -1.0],
+              8: [-9.0, 128.0, -1008.0, 8064.0, -14350.0, 8064.0, -1008.0, 128.0, -9.0]}[order]
+    B = len(coeffs) // 2
+    xb, xe, yb, ye = region
+    out = prev.clone()
+    c = prev[yb:ye, xb:xe]
+    dx = torch.zeros_like(c)
+    dy = torch.zeros_like(c)
+    for k, w in enumerate(coeffs):
+        o = k - B
+        dx = dx + w * prev[yb:ye, xb + o:xe + o]
+        dy = dy + w * prev[yb + o:ye + o, xb:xe]
+    out[yb:ye, xb:xe] = c + xcfl * dx + ycfl * dy
+    return out

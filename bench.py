@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: distributed 2-D heat-diffusion stencil, 16384^2 global
+grid, order 8, fp32, RCCL halo exchange over xGMI (BASELINE.json config #5).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+launched under torch.distributed.run (one rank per GPU). W untimed steps, then
+EXACTLY K timed steps bracketed by barrier + synchronize, max over ranks; rank
+0 prints one JSON line.
+
+A "step" is one full timestep of the global grid: the FTCS sweep of every
+point plus the halo exchange between neighbouring ranks (1-D stripes, async
+mode: deep interior overlapped with the exchange, borders after it).
+
+Metric convention: effective GB/s = points x 72 B (17 taps + 1
+store, fp32) per iteration / time -- the convention the reference's 240 GB/s
+(hw2, 4000^2, order 8, LDS kernel, Fermi) is quoted in. Also reported: the
+minimum-traffic HBM rate (8 B/pt) and its % of 8 TB/s per GPU. Strong scaling:
+the global grid is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_GBPS = 239.7  # heat 4000^2 order 8 LDS kernel, 48.07 ms / 10 iters, 72 B/pt
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--order", type=int, default=8)
+    ap.add_argument("--method", type=int, default=1, help="1 = 1-D stripes, 2 = 2-D blocks")
+    ap.add_argument("--mode", choices=["async", "sync"], default="async")
+    ap.add_argument("--variant", default="stream")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import cme213x
+    from cme213x.models.heat2d import bytes_per_point
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import init_from_env
+    from cme213x.utils.params import SimParams
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch under torch.distributed.run",
+                  file=sys.stderr)
+            return 2
+    comm = init_from_env("cuda")
+    rank = comm.rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
+                  grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
+    sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant)
+
+    def barrier_sync():
+        torch.cuda.synchronize(dev)
+        comm.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        sim.step()
+    sim.finish()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.step()
+    sim.finish()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    comm.allreduce_(elapsed, "max")
+    secs = float(elapsed.item())
+
+    # sanity: the solution must stay finite and within the BC/IC bounds
+    local = next(iter(sim.subs.values())).grid
+    st = local.buf[local.cur]
+    bad = torch.tensor([float(~torch.isfinite(st).all()) + float(st.abs().max() > 1e3)], device=dev)
+    comm.allreduce_(bad, "max")
+
+    pts = args.n * args.n
+    bpp = bytes_per_point(args.order, torch.float32)
+    eff = pts * bpp * args.steps / secs / 1e9
+    hbm = pts * 8 * args.steps / secs / 1e9
+    ms = secs * 1e3 / args.steps
+    if rank == 0:
+        rec = {
+            "metric": "effective GB/s (2-D heat stencil, order 8, fp32, 72 B/pt reference model)",
+            "value": round(eff, 2),
+            "unit": "GB/s",
+            "n_gpus": args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(eff / BASELINE_GBPS, 2),
+            "dtype": "fp32",
+            "data": "synthetic (uniform IC 5.0, Dirichlet BCs 0/10/0/10)",
+            "config": {
+                "model": f"heat2d-{args.n}x{args.n}-order{args.order} (BASELINE.json config #5)",
+                "global_batch": pts,
+                "seq_len": 1,
+                "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
+                "variant": args.variant,
+            },
+            "hbm_GBps_min_traffic": round(hbm, 1),
+            "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),
+            "gpoints_per_s": round(pts * args.steps / secs / 1e9, 2),
+            "sanity_ok": bool(bad.item() == 0),
+        }
+        print(json.dumps(rec), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

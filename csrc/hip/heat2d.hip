@@ -1,0 +1,279 @@
+// 2-D heat diffusion (explicit FTCS), orders 2/4/8, fp32/fp64, on gfx950.
+//
+// Capability parity with the reference's single-GPU hw2 kernels
+// (hw/hw2/solution/2dHeat_solution.cu:413-530 global + gpuShared) and the
+// distributed hw5 compute loops (hw/hw5/2dHeat_solution.cpp:501-628), which
+// are expressed here as one kernel family over an arbitrary compute REGION so
+// the same code serves full sweeps, async "interior only" sweeps and the
+// border strips computed after the halo exchange.
+//
+// Device grid layout: rows of `pitch` elements (pitch % 64 == 0, pitch >= gx),
+// row y at base + y*pitch; the region [xb,xe) x [yb,ye) is updated from prev.
+//
+// Three variants (the lecture's optimisation ladder, re-derived for wave64):
+//   naive  : 1 thread / point, 64x4 blocks, every neighbour a global load.
+//   lds    : 2-D LDS tile (64+2B) x (TY+2B) with +1 padding, 4 waves, each
+//            thread marches TY/4 rows (the reference's gpuShared idea).
+//   stream : register sliding window. Each wave owns a 248-column strip
+//            (62 output lanes + 1 halo lane per side, 4 elements per lane =
+//            16 B fp32 / 32 B fp64 accesses) and marches down `chunk` rows,
+//            holding the 2B+1 row window in VGPRs. x-neighbours come from the
+//            adjacent lanes through DPP wave_shr/wave_shl (no LDS), and the
+//            next RB rows are prefetched while the current RB are computed.
+//            Each input element is fetched from HBM ~once: 8 B/pt fp32.
+#include "cme213/common.h"
+#include "cme213/heat_stencil.h"
+#include "cme213/vec.h"
+
+using namespace cme;
+
+// ---------------------------------------------------------------- naive
+template <typename T, int ORDER>
+__global__ __launch_bounds__(256) void heat_naive_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+                                                         int xb, int xe, int yb, int ye, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    const int x = xb + (int)(blockIdx.x * 64 + threadIdx.x % 64);
+    const int y = yb + (int)(blockIdx.y * 4 + threadIdx.x / 64);
+    if (x >= xe || y >= ye) return;
+    const T* p = prev + (size_t)y * pitch + x;
+    T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        xm[k] = p[-(k + 1)];
+        xp[k] = p[k + 1];
+        ym[k] = p[-(ptrdiff_t)(k + 1) * pitch];
+        yp[k] = p[(ptrdiff_t)(k + 1) * pitch];
+    }
+    curr[(size_t)y * pitch + x] = heat_update<ORDER>(p[0], xm, xp, ym, yp, xcfl, ycfl);
+}
+
+// ---------------------------------------------------------------- lds tile
+// Block: 256 threads = 64 columns x 4 row-groups; tile TX=64 x TY rows.
+template <typename T, int ORDER, int TY, int PAD>
+__global__ __launch_bounds__(256) void heat_lds_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+                                                       int gy, int xb, int xe, int yb, int ye, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int TX = 64;
+    constexpr int LW = TX + 2 * B + PAD;  // LDS row length (PAD breaks the power-of-2 stride)
+    constexpr int LH = TY + 2 * B;
+    __shared__ T tile[LH * LW];
+    const int tx = threadIdx.x % 64, ty = threadIdx.x / 64;
+    const int x0 = xb + (int)blockIdx.x * TX;
+    const int y0 = yb + (int)blockIdx.y * TY;
+    // Cooperative load of the haloed tile (rows/cols outside the allocation are
+    // clamped; they only feed points outside the region).
+    for (int i = threadIdx.x; i < LH * (TX + 2 * B); i += 256) {
+        const int r = i / (TX + 2 * B), c = i % (TX + 2 * B);
+        int gyy = y0 - B + r;
+        int gxx = x0 - B + c;
+        gyy = gyy < 0 ? 0 : (gyy >= gy ? gy - 1 : gyy);
+        gxx = gxx < 0 ? 0 : (gxx >= pitch ? pitch - 1 : gxx);
+        tile[r * LW + c] = prev[(size_t)gyy * pitch + gxx];
+    }
+    __syncthreads();
+    const int x = x0 + tx;
+    if (x >= xe) return;
+#pragma unroll 4
+    for (int r = ty; r < TY; r += 4) {
+        const int y = y0 + r;
+        if (y >= ye) break;
+        const T* t = &tile[(r + B) * LW + tx + B];
+        T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            xm[k] = t[-(k + 1)];
+            xp[k] = t[k + 1];
+            ym[k] = t[-(k + 1) * LW];
+            yp[k] = t[(k + 1) * LW];
+        }
+        curr[(size_t)y * pitch + x] = heat_update<ORDER>(t[0], xm, xp, ym, yp, xcfl, ycfl);
+    }
+}
+
+// ---------------------------------------------------------------- stream
+constexpr int kStripOut = 62 * 4;  // output columns per wave strip
+
+template <typename T, int ORDER, int RB>
+__global__ __launch_bounds__(256) void heat_stream_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+                                                          int gy, int xb, int xe, int yb, int ye, int strips, int chunk,
+                                                          int total_waves, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int NW = RB + 2 * B;  // rows held in the window
+    const int lane = lane_id();
+    const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
+    if (wave >= total_waves) return;
+    const int strip = wave % strips;
+    const int ck = wave / strips;
+    const int y0 = yb + ck * chunk;
+    const int y1 = min(ye, y0 + chunk);
+    const int xs = (xb & ~3) + strip * kStripOut;
+    const int xbase = xs - 4 + 4 * lane;
+    const int xl = min(max(xbase, 0), pitch - 4);
+    const bool out_lane = (lane >= 1) && (lane <= 62) && (xbase < xe) && (xbase + 4 > xb);
+    const bool full_vec = (xbase >= xb) && (xbase + 4 <= xe);
+    const T* src = prev + xl;
+    T* dst = curr + xl;
+
+    auto row_ptr = [&](int r) -> const T* {
+        r = r < 0 ? 0 : (r >= gy ? gy - 1 : r);
+        return src + (size_t)r * pitch;
+    };
+
+    V4<T> win[NW];
+    V4<T> nxt[RB];
+#pragma unroll
+    for (int i = 0; i < 2 * B; ++i) win[i] = load4(row_ptr(y0 - B + i));
+#pragma unroll
+    for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(y0 + B + i));
+
+    for (int y = y0; y < y1; y += RB) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) win[2 * B + i] = nxt[i];
+        if (y + RB < y1) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(y + RB + B + i));
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            const V4<T> c = win[r + B];
+            const V4<T> L = wave_shr1(c);  // lane-1's 4 columns
+            const V4<T> R = wave_shl1(c);  // lane+1's 4 columns
+            T row[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                row[j] = L[j];
+                row[4 + j] = c[j];
+                row[8 + j] = R[j];
+            }
+            V4<T> o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+                for (int k = 0; k < B; ++k) {
+                    xm[k] = row[4 + j - (k + 1)];
+                    xp[k] = row[4 + j + (k + 1)];
+                    ym[k] = win[r + B - (k + 1)][j];
+                    yp[k] = win[r + B + (k + 1)][j];
+                }
+                o[j] = heat_update<ORDER>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+            }
+            const int yy = y + r;
+            if (out_lane && yy < y1) {
+                T* d = dst + (size_t)yy * pitch;
+                if (full_vec) {
+                    store4(d, o);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (xbase + j >= xb && xbase + j < xe) d[j] = o[j];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2 * B; ++i) win[i] = win[RB + i];
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+namespace {
+
+struct Region {
+    int xb, xe, yb, ye;
+};
+
+template <typename T, int ORDER>
+int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, int chunk_hint,
+                hipStream_t s) {
+    const int W = g.xe - g.xb, H = g.ye - g.yb;
+    if (W <= 0 || H <= 0) return 0;
+    if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
+    if (variant == 0) {
+        dim3 grid(cdiv(W, 64), cdiv(H, 4));
+        hipLaunchKernelGGL((heat_naive_kernel<T, ORDER>), grid, dim3(256), 0, s, prev, curr, pitch, g.xb, g.xe, g.yb,
+                           g.ye, xcfl, ycfl);
+    } else if (variant == 1) {
+        constexpr int TY = 32;
+        dim3 grid(cdiv(W, 64), cdiv(H, TY));
+        hipLaunchKernelGGL((heat_lds_kernel<T, ORDER, TY, 1>), grid, dim3(256), 0, s, prev, curr, pitch, gy, g.xb,
+                           g.xe, g.yb, g.ye, xcfl, ycfl);
+    } else if (variant == 3) {
+        // LDS tile without the +1 pad (bank-conflict study arm).
+        constexpr int TY = 32;
+        dim3 grid(cdiv(W, 64), cdiv(H, TY));
+        hipLaunchKernelGGL((heat_lds_kernel<T, ORDER, TY, 0>), grid, dim3(256), 0, s, prev, curr, pitch, gy, g.xb,
+                           g.xe, g.yb, g.ye, xcfl, ycfl);
+    } else {
+        constexpr int RB = sizeof(T) == 4 ? 8 : 4;
+        const int x_lo = g.xb & ~3;
+        const int strips = (int)cdiv(g.xe - x_lo, kStripOut);
+        // Enough waves to fill 256 CUs x 16 waves, chunk a multiple of RB.
+        int chunk = chunk_hint;
+        if (chunk <= 0) {
+            const long target_waves = 256L * 16;
+            long rows = ((long)strips * H + target_waves - 1) / target_waves;
+            rows = rows < RB ? RB : rows;
+            rows = rows > 512 ? 512 : rows;
+            chunk = (int)rows;
+        }
+        chunk = ((chunk + RB - 1) / RB) * RB;
+        const int chunks = (int)cdiv(H, chunk);
+        const int total_waves = strips * chunks;
+        hipLaunchKernelGGL((heat_stream_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
+                           pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
+    }
+    CME_LAUNCH_STATUS();
+}
+
+template <typename T>
+int dispatch_heat(int order, int variant, const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl,
+                  int chunk, hipStream_t s) {
+    switch (order) {
+        case 2: return launch_heat<T, 2>(variant, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 4: return launch_heat<T, 4>(variant, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 8: return launch_heat<T, 8>(variant, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+// variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad)
+CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
+                                 int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
+    return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
+                                as_stream(stream));
+}
+
+CME_EXPORT int cme_heat_step_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
+                                 int order, int variant, double xcfl, double ycfl, int chunk, void* stream) {
+    return dispatch_heat<double>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
+                                 as_stream(stream));
+}
+
+// Multi-step driver: `iters` ping-pong sweeps of the full region in one call
+// (buffers a/b, first sweep reads a). Avoids per-iteration host round trips
+// (the reference synchronises after every launch: 2dHeat_solution.cu:549).
+CME_EXPORT int cme_heat_run_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
+                                int variant, float xcfl, float ycfl, int iters, int chunk, void* stream) {
+    for (int i = 0; i < iters; ++i) {
+        const float* p = (i & 1) ? b : a;
+        float* c = (i & 1) ? a : b;
+        int rc = dispatch_heat<float>(order, variant, p, c, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
+                                      as_stream(stream));
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+CME_EXPORT int cme_heat_run_f64(double* a, double* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
+                                int variant, double xcfl, double ycfl, int iters, int chunk, void* stream) {
+    for (int i = 0; i < iters; ++i) {
+        const double* p = (i & 1) ? b : a;
+        double* c = (i & 1) ? a : b;
+        int rc = dispatch_heat<double>(order, variant, p, c, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
+                                       as_stream(stream));
+        if (rc) return rc;
+    }
+    return 0;
+}

@@ -1,0 +1,55 @@
+// cme213x native runtime: shared definitions for the HIP (gfx950) library.
+//
+// Replaces the reference's per-assignment `mp1-util.h` launch checking
+// (hw/hw1/programming/mp1-util.h:8-18: sync + cudaGetLastError + exit) with a
+// non-fatal, graph-capturable contract: every exported launcher returns the
+// hipError_t as an int and never synchronises, so the Python layer can raise a
+// RuntimeError and callers can capture launches into hipGraphs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CME_EXPORT extern "C" __attribute__((visibility("default")))
+
+// Wave64 is the CDNA execution quantum; never assume 32.
+constexpr int kWave = 64;
+// MI355X: 256 CUs in 8 XCDs.
+constexpr int kNumCU = 256;
+constexpr int kNumXCD = 8;
+
+#define CME_TRY(expr)                                  \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return (int)_e;          \
+    } while (0)
+
+// Return the launch status without synchronising (check_launch replacement).
+#define CME_LAUNCH_STATUS() return (int)hipGetLastError()
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+// Grid size for grid-stride memory-bound kernels: enough blocks to fill all
+// 256 CUs several times over, capped so the tail stays short.
+static inline unsigned stream_grid(size_t work_items, unsigned block, unsigned blocks_per_cu = 8) {
+    size_t want = (work_items + block - 1) / block;
+    size_t cap = (size_t)kNumCU * blocks_per_cu;
+    if (want > cap) want = cap;
+    if (want < 1) want = 1;
+    return (unsigned)want;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must
+// be bijective"): blocks b and b+8 share an XCD under round-robin dispatch, so
+// give each XCD group a contiguous range of logical tiles. Speed only, never
+// correctness.
+__device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned nwg) {
+    const unsigned xcd = bid % kNumXCD;
+    const unsigned q = nwg / kNumXCD, r = nwg % kNumXCD;
+    const unsigned base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + bid / kNumXCD;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }

@@ -1,0 +1,79 @@
+"""Multi-process (gloo, CPU) tests of the distributed heat solver and the
+communicator layer: the same code path the 8-GPU RCCL run uses."""
+import numpy as np
+import pytest
+import torch
+
+from dist_util import run_ranks
+
+
+def _heat_rank(rank, world, method, sync, order):
+    import cme213x
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
+                  sync=sync, flavor="hw5")
+    sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive")
+    # non-uniform initial condition (same on every rank, by global coords)
+    for s in sim.subs.values():
+        g, b = s.grid, s.blk
+        B = g.B
+        yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+        ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0)
+        g.buf[:, B:B + b.ny, B:B + b.nx] = ic
+    sim.exchange(sim._cur()).wait()
+    sim.run(p.iters)
+    s = next(iter(sim.subs.values()))
+    B = s.grid.B
+    return (s.blk.x0, s.blk.y0, s.grid.state()[B:B + s.blk.ny, B:B + s.blk.nx])
+
+
+def _single(method, order, sync):
+    import cme213x
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
+                  sync=sync, flavor="hw5")
+    sim = DistHeat(p, None, torch.float64, "cpu", variant="naive")
+    g = sim.subs[0].grid
+    B = g.B
+    yy, xx = np.meshgrid(np.arange(p.ny), np.arange(p.nx), indexing="ij")
+    g.buf[:, B:B + p.ny, B:B + p.nx] = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0)
+    sim.run(p.iters)
+    return g.state()[B:-B, B:-B]
+
+
+@pytest.mark.parametrize("method,sync,order,world", [(1, True, 8, 2), (1, False, 4, 2), (2, False, 8, 4),
+                                                     (2, True, 2, 4)])
+def test_dist_heat_matches_single(method, sync, order, world):
+    parts = run_ranks(_heat_rank, world, (method, sync, order))
+    ref = _single(method, order, sync)
+    for x0, y0, st in parts:
+        np.testing.assert_array_equal(st, ref[y0:y0 + st.shape[0], x0:x0 + st.shape[1]])
+
+
+def _collectives(rank, world):
+    from cme213x.parallel.comm import TorchComm
+
+    c = TorchComm()
+    t = torch.tensor([float(rank + 1)])
+    c.allreduce_(t)
+    g = c.allgather(torch.tensor([rank]))
+    b = c.broadcast_(torch.tensor([rank * 10]), src=1)
+    sub = c.split(color=rank % 2)
+    s = sub.allreduce_(torch.tensor([1.0]))
+    a2a = c.alltoall(torch.arange(world, dtype=torch.float32) + 100 * rank)
+    return (t.item(), g.tolist(), b.item(), sub.size, s.item(), a2a.tolist())
+
+
+def test_collectives_gloo():
+    out = run_ranks(_collectives, 4)
+    for r, (ar, ag, bc, ssz, ss, a2a) in enumerate(out):
+        assert ar == 10.0
+        assert ag == [[0], [1], [2], [3]]
+        assert bc == 10
+        assert ssz == 2 and ss == 2.0
+        assert a2a == [float(r + 100 * k) for k in range(4)]
