@@ -1,1 +1,1 @@
-from . import heat2d, heat2d_dist  # noqa: F401
+from . import heat2d, heat2d_dist, cipher, pagerank  # noqa: F401

@@ -93,14 +93,14 @@ __global__ __launch_bounds__(256) void heat_lds_kernel(const T* __restrict__ pre
 // ---------------------------------------------------------------- stream
 constexpr int kStripOut = 62 * 4;  // output columns per wave strip
 
-template <typename T, int ORDER, int RB>
-__global__ __launch_bounds__(256) void heat_stream_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+template <typename T, int ORDER, int RB, int WPB = 4, bool NT = false>
+__global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
                                                           int gy, int xb, int xe, int yb, int ye, int strips, int chunk,
                                                           int total_waves, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
     constexpr int NW = RB + 2 * B;  // rows held in the window
     const int lane = lane_id();
-    const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
+    const int wave = (int)blockIdx.x * WPB + (int)(threadIdx.x / 64);
     if (wave >= total_waves) return;
     const int strip = wave % strips;
     const int ck = wave / strips;
@@ -162,7 +162,13 @@ __global__ __launch_bounds__(256) void heat_stream_kernel(const T* __restrict__ 
             if (out_lane && yy < y1) {
                 T* d = dst + (size_t)yy * pitch;
                 if (full_vec) {
-                    store4(d, o);
+                    if constexpr (NT && sizeof(T) == 4) {
+                        typedef float f32x4 __attribute__((ext_vector_type(4)));
+                        f32x4 ov = {o[0], o[1], o[2], o[3]};
+                        __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(d));
+                    } else {
+                        store4(d, o);
+                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
@@ -276,4 +282,55 @@ CME_EXPORT int cme_heat_run_f64(double* a, double* b, int pitch, int gy, int xb,
         if (rc) return rc;
     }
     return 0;
+}
+
+// Tuning entry point for the streaming kernel (order 8, fp32): explores rows
+// per register block (rb 4/8/12), waves per block (4/8/16) and non-temporal
+// stores. Used by benchmarks/tune_heat.py; the production path is variant 2.
+namespace {
+template <int RB, int WPB, bool NT>
+int tune_launch(const float* prev, float* curr, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk,
+                hipStream_t s) {
+    const int H = g.ye - g.yb;
+    const int x_lo = g.xb & ~3;
+    const int strips = (int)cdiv(g.xe - x_lo, kStripOut);
+    if (chunk <= 0) {
+        long rows = ((long)strips * H + 4095) / 4096;
+        chunk = (int)(rows < RB ? RB : (rows > 512 ? 512 : rows));
+    }
+    chunk = ((chunk + RB - 1) / RB) * RB;
+    const int total_waves = strips * (int)cdiv(H, chunk);
+    hipLaunchKernelGGL((heat_stream_kernel<float, 8, RB, WPB, NT>), dim3(cdiv(total_waves, WPB)), dim3(WPB * 64), 0,
+                       s, prev, curr, pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
+    CME_LAUNCH_STATUS();
+}
+template <int RB, int WPB>
+int tune_nt(int nt, const float* prev, float* curr, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk,
+            hipStream_t s) {
+    return nt ? tune_launch<RB, WPB, true>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s)
+              : tune_launch<RB, WPB, false>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+}
+template <int RB>
+int tune_wpb(int wpb, int nt, const float* prev, float* curr, int pitch, int gy, Region g, float xcfl, float ycfl,
+             int chunk, hipStream_t s) {
+    switch (wpb) {
+        case 4: return tune_nt<RB, 4>(nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 8: return tune_nt<RB, 8>(nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 16: return tune_nt<RB, 16>(nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_stream_tune_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb,
+                                        int ye, float xcfl, float ycfl, int rb, int wpb, int nt, int chunk,
+                                        void* stream) {
+    Region g{xb, xe, yb, ye};
+    hipStream_t s = as_stream(stream);
+    switch (rb) {
+        case 4: return tune_wpb<4>(wpb, nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 8: return tune_wpb<8>(wpb, nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        case 12: return tune_wpb<12>(wpb, nt, prev, curr, pitch, gy, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
 }
