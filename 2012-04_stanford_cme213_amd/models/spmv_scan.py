@@ -1,0 +1,186 @@
+"""Final project: the iterated segmented "SpMV-scan".
+
+Problem (``hw/hw_final/Final.pdf``; reference checker
+``hw/hw_final/programming/aux/reference_spMVscan-released.cu:38-54``):
+repeat N times ``b_j = sum_{l=s_i}^{j} a_l * x[k_l]`` for j in segment
+``[s_i, s_{i+1})``, then ``a <- b``.
+
+MI355X design (vs. the reference's one-32-lane-warp-per-segment kernel,
+``fp.cu:28-59``, which is racy on anything but lock-step Fermi and loses badly
+on short segments): x is pre-gathered once (``xx = x[k]``, outside the timed
+region, as the rules allow -- ``fp.cu:124-125``), segment heads become a 1-bit
+mask, and each iteration is ONE single-pass kernel: 16-B loads of a and xx,
+fused multiply, DPP segmented wave scans, decoupled look-back across 4096-
+element tiles whose walk stops at the first tile containing a head. Traffic:
+12 B/element/iteration + n/8 B of flags -- independent of segment lengths.
+
+I/O parity: ``a.txt`` (``n p q N`` / a[n] / s[p] / k[n]), ``x.txt`` (x[q]),
+``b.txt`` (``v `` per element), the line ``"The running time of my code for
+<N> iterations is: <ms> milliseconds."`` and the checker's L2 / Linf errors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops.scan import head_flags_from_offsets, segmented_scan
+from ..utils.gridio import write_vector
+from ..utils.timer import EventTimer
+
+
+@dataclass
+class SpmvScanProblem:
+    a: np.ndarray  # float32 [n]
+    s: np.ndarray  # int32 [p]   (s[0] = 0, s[p-1] = n)
+    k: np.ndarray  # int32 [n]   (0 <= k < q)
+    x: np.ndarray  # float32 [q]
+    iters: int
+
+    @property
+    def n(self) -> int:
+        return self.a.size
+
+    @property
+    def p(self) -> int:
+        return self.s.size
+
+    @property
+    def q(self) -> int:
+        return self.x.size
+
+    def validate(self) -> None:
+        """The loader's invariants (``aux/mp1-util.h:104-147``)."""
+        assert self.s[0] == 0 and self.s[-1] == self.n, "s must start at 0 and end at n"
+        assert np.all(np.diff(self.s) > 0), "s must be strictly increasing"
+        assert self.k.min() >= 0 and self.k.max() < self.q, "k out of range"
+
+
+def load(a_path: str, x_path: str) -> SpmvScanProblem:
+    tok = np.fromfile(a_path, sep=" ")
+    n, p, q, N = (int(v) for v in tok[:4])
+    a = tok[4:4 + n].astype(np.float32)
+    s = tok[4 + n:4 + n + p].astype(np.int64).astype(np.int32)
+    k = tok[4 + n + p:4 + n + p + n].astype(np.int64).astype(np.int32)
+    x = np.fromfile(x_path, sep=" ")[:q].astype(np.float32)
+    prob = SpmvScanProblem(a, s, k, x, N)
+    prob.validate()
+    return prob
+
+
+def save(prob: SpmvScanProblem, a_path: str, x_path: str) -> None:
+    with open(a_path, "w") as f:
+        f.write(f"{prob.n} {prob.p} {prob.q} {prob.iters}\n")
+        f.write(" ".join(repr(float(v)) for v in prob.a) + " \n")
+        f.write(" ".join(str(int(v)) for v in prob.s) + "\n")
+        f.write(" ".join(str(int(v)) for v in prob.k) + " \n")
+    with open(x_path, "w") as f:
+        f.write(" ".join(repr(float(v)) for v in prob.x) + " \n")
+
+
+def generate(n: int, p: int, q: int, iters: int, seed: int = 0, values: np.ndarray | None = None) -> SpmvScanProblem:
+    """readMM.py's generator (``aux/readMM.py:16-61``): s = 0, a sorted random
+    sample of size p (its first element dropped), n; k ~ U[0, q); x ~ U(-1, 1).
+    ``values`` (the matrix entries) default to U(-1, 1) -- the benchmark
+    matrices themselves are not in the reference repo."""
+    rng = np.random.default_rng(seed)
+    a = values.astype(np.float32) if values is not None else rng.uniform(-1, 1, n).astype(np.float32)
+    samp = np.sort(rng.choice(n, size=p, replace=False))
+    s = np.empty(p, dtype=np.int32)
+    s[0] = 0
+    s[1:p - 1] = samp[1:p - 1]
+    s[p - 1] = n
+    k = rng.integers(0, q, size=n, dtype=np.int64).astype(np.int32)
+    x = rng.uniform(-1, 1, q).astype(np.float32)
+    return SpmvScanProblem(a, s, k, x, iters)
+
+
+# (n, p, N) of the 15 benchmark matrices (from the checker log)
+BENCH_SHAPES = {
+    "cant": (4007383, 62450, 50), "consph": (6010480, 83333, 20), "cop20k_A": (2624331, 121191, 73),
+    "dense2": (4000000, 1999, 10), "jonheart": (37035, 3128, 60), "mac_econ_fwd500": (1273389, 206499, 12),
+    "mc2depi": (2100225, 525824, 70), "pdb1HYS": (4344765, 36416, 30), "pwtk": (11634424, 217917, 25),
+    "qcd5_4": (1916928, 49151, 63), "rail4284": (11279748, 4283, 10), "rma10": (2374001, 46834, 74),
+    "scircuit": (958936, 170997, 30), "shipsec1": (7813404, 140873, 10), "webbase-1M": (3105536, 1000004, 77),
+}
+# GTX 580 ms for each (Final_Report_DongBang_Tsai.tex:237-251)
+REF_MS = {"cant": 107.911, "consph": 62.117, "cop20k_A": 146.603, "dense2": 26.676, "jonheart": 2.665,
+          "mac_econ_fwd500": 23.544, "mc2depi": 302.068, "pdb1HYS": 63.582, "pwtk": 158.697, "qcd5_4": 74.608,
+          "rail4284": 58.752, "rma10": 99.947, "scircuit": 47.816, "shipsec1": 42.401, "webbase-1M": 592.115}
+
+
+class SpmvScanSolver:
+    """Device-resident state: a (updated in place), xx = x[k], head bitmask."""
+
+    def __init__(self, prob: SpmvScanProblem, device="cuda"):
+        self.prob = prob
+        self.device = torch.device(device)
+        x = torch.from_numpy(prob.x).to(self.device)
+        k = torch.from_numpy(prob.k.astype(np.int64)).to(self.device)
+        self.xx = x[k].contiguous()  # pre-flattened gather (untimed, fp.cu:124-125)
+        self.flags = head_flags_from_offsets(torch.from_numpy(prob.s), prob.n, self.device)
+        self.a = torch.from_numpy(prob.a.copy()).to(self.device)
+
+    def reset(self) -> None:
+        self.a.copy_(torch.from_numpy(self.prob.a))
+
+    def step(self) -> None:
+        segmented_scan(self.a, self.flags, out=self.a, mul=self.xx)
+
+    def run(self, iters: int | None = None) -> torch.Tensor:
+        for _ in range(self.prob.iters if iters is None else iters):
+            self.step()
+        return self.a
+
+
+def reference_solution(prob: SpmvScanProblem, iters: int | None = None) -> np.ndarray:
+    """fp64 serial result (the instructor checker's algorithm), vectorised:
+    per iteration, a segmented cumulative sum of a*x[k] in double."""
+    a = prob.a.astype(np.float64)
+    xx = prob.x.astype(np.float64)[prob.k]
+    starts = prob.s[:-1].astype(np.int64)
+    seg_id = np.repeat(np.arange(starts.size), np.diff(prob.s.astype(np.int64)))
+    for _ in range(prob.iters if iters is None else iters):
+        v = a * xx
+        c = np.cumsum(v)
+        base = np.concatenate([[0.0], c])[starts]  # cumsum just before each segment start
+        a = c - base[seg_id]
+    return a
+
+
+def errors(ref: np.ndarray, b: np.ndarray) -> dict:
+    """The checker's metrics (``reference_spMVscan-released.cu:64-144``)."""
+    ref = ref.astype(np.float64)
+    b = b.astype(np.float64)
+    d = ref - b
+    l2 = float(np.sqrt(np.dot(d, d)))
+    na = float(np.sqrt(np.dot(ref, ref)))
+    linf = float(np.abs(d).max())
+    ninf = float(np.abs(ref).max())
+    return {"L2": l2, "relL2": l2 / na if na > 0 else float("inf"), "Linf": linf,
+            "relLinf": linf / ninf if ninf > 0 else float("inf")}
+
+
+def run_fp(a_path: str, x_path: str, cpu_check: bool = False, device: str | None = None,
+           out_path: str = "b.txt") -> dict:
+    """The ``./fp a.txt x.txt [check]`` driver (``fp.cu:74-216``)."""
+    device = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    prob = load(a_path, x_path)
+    print(f"\nDim of a: {prob.n}\nDim of x: {prob.q}\nDim of s: {prob.p}\n# of iters: {prob.iters}\n")
+    sol = SpmvScanSolver(prob, device)
+    sol.run(1)  # warm-up (code object load), then restore a
+    sol.reset()
+    t = EventTimer("spmv-scan", device=device if device != "cpu" else None, print_result=False)
+    with t:
+        sol.run()
+    print(f"The running time of my code for {prob.iters} iterations is: {t.ms:g} milliseconds.\n")
+    b = sol.a.cpu().numpy()
+    res = {"ms": t.ms, "n": prob.n, "p": prob.p, "N": prob.iters,
+           "GBps": 12.0 * prob.n * prob.iters / t.ms / 1e6}
+    if cpu_check:
+        ref = reference_solution(prob)
+        res.update(errors(ref, b))
+        write_vector("b_cpu.txt", ref.astype(np.float32))
+    write_vector(out_path, b)
+    return res

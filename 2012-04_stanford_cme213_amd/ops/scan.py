@@ -1,0 +1,123 @@
+"""Scan / reduction / segmented-scan ops.
+
+* :func:`scan` -- single-pass decoupled look-back (default) or the lecture's
+  multi-level scan-then-add with a Blelloch or Hillis-Steele block algorithm
+  (``slides/Lecture16.pdf``; ``my-refs/scan.pdf`` Fig. 5).
+* :func:`reduce` -- sum / max / min; the lecture's shared-memory tree
+  (``slides/Lecture05.pdf`` 15-16) as ``algo="tree"``.
+* :func:`segmented_scan` -- inclusive, head-flag segmented scan (Lecture21;
+  nvr-2008-003), optionally fused with an element-wise multiply: the final
+  project's ``a *= x[k]; b = segscan(a)`` step (``hw/hw_final/programming/
+  fp.cu:168-185``) in one pass.
+
+CPU tensors use the OpenMP oracles in ``csrc/cpu/scan_cpu.cpp``.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+_ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_scan_mlevel", "ppqiiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_reduce", "pqiiippp")
+_ext.proto(_ext.HIP_PROTOS, "cme_segscan", "pppppiqpp")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_scan", "ppqii")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_reduce", "pqiip")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_segscan", "ppppiq")
+
+_DT = {torch.float32: 0, torch.int32: 1}
+_DT_SCAN = {torch.float32: 0, torch.int32: 1, torch.uint32: 2}
+_OPS = {"sum": 0, "max": 1, "min": 2}
+TILE = 4096
+
+_ws_cache: dict = {}
+
+
+def workspace(device: torch.device, nbytes: int, key: str = "lookback") -> torch.Tensor:
+    """Per-device scratch, grown on demand (never allocated inside a launch)."""
+    k = (key, device.index)
+    t = _ws_cache.get(k)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+        _ws_cache[k] = t
+    return t
+
+
+def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
+    tiles = (x.numel() + TILE - 1) // TILE
+    return workspace(x.device, tiles * 8 + 16)
+
+
+def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
+         algo: str = "lookback") -> torch.Tensor:
+    """Prefix sum of a 1-D contiguous float32/int32/uint32 tensor.
+    algo: "lookback" (single pass), "blelloch" or "hillis" (multi-level)."""
+    if not x.is_contiguous():
+        x = x.contiguous()
+    out = torch.empty_like(x) if out is None else out
+    n = x.numel()
+    if x.is_cuda:
+        s = _ext.stream_ptr(x.device)
+        if algo == "lookback":
+            _ext.call_hip("cme_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
+                          _lookback_ws(x).data_ptr(), s)
+        else:
+            if out.data_ptr() == x.data_ptr() and not exclusive:
+                raise ValueError("in-place inclusive multi-level scan is not supported")
+            levels, b = 0, (n + 511) // 512
+            while b > 1:
+                levels += b
+                b = (b + 511) // 512
+            ws = workspace(x.device, (levels + 1) * 4, "mlevel")
+            _ext.call_hip("cme_scan_mlevel", x.data_ptr(), out.data_ptr(), n, _DT[x.dtype],
+                          0 if algo == "blelloch" else 1, int(exclusive), ws.data_ptr(), s)
+    else:
+        _ext.call_cpu("cme_cpu_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive))
+    return out
+
+
+def reduce(x: torch.Tensor, op: str = "sum", algo: str = "vector") -> torch.Tensor:
+    """Full reduction of a float32/int32 tensor; returns a 0-d tensor on x's device."""
+    x = x.contiguous()
+    out = torch.empty((), dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        part = workspace(x.device, 2048 * 4, "reduce")
+        _ext.call_hip("cme_reduce", x.data_ptr(), x.numel(), _DT[x.dtype], _OPS[op], 0 if algo == "vector" else 1,
+                      part.data_ptr(), out.data_ptr(), _ext.stream_ptr(x.device))
+    else:
+        _ext.call_cpu("cme_cpu_reduce", x.data_ptr(), x.numel(), _DT[x.dtype], _OPS[op], out.data_ptr())
+    return out
+
+
+def head_flags_from_offsets(s: torch.Tensor, n: int, device=None, bitmask: bool = True) -> torch.Tensor:
+    """Segment heads from the final project's offset array ``s`` (s[0] = 0,
+    s[p-1] = n, strictly increasing; segment i = [s[i-1], s[i])). Returns a
+    bitmask (int32 words, bit i%32 of word i/32) or a uint8 per element."""
+    heads = s[:-1].to(torch.int64)
+    if bitmask:
+        words = torch.zeros((n + 31) // 32, dtype=torch.int64)
+        w = heads // 32
+        bit = torch.ones_like(heads) << (heads % 32)
+        words.index_add_(0, w, bit)  # heads are distinct: add == or
+        words = torch.where(words >= 2**31, words - 2**32, words).to(torch.int32)
+        return words.to(device) if device is not None else words
+    f = torch.zeros(n, dtype=torch.uint8)
+    f[heads] = 1
+    return f.to(device) if device is not None else f
+
+
+def segmented_scan(x: torch.Tensor, flags: torch.Tensor, out: torch.Tensor | None = None,
+                   mul: torch.Tensor | None = None) -> torch.Tensor:
+    """Inclusive segmented sum scan of float32 ``x`` (optionally ``x*mul``).
+    ``flags``: uint8 per element (0/1) or int32 bitmask words."""
+    out = torch.empty_like(x) if out is None else out
+    n = x.numel()
+    mode = 0 if flags.dtype == torch.uint8 else 1
+    mp = mul.data_ptr() if mul is not None else None
+    if x.is_cuda:
+        _ext.call_hip("cme_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n,
+                      _lookback_ws(x).data_ptr(), _ext.stream_ptr(x.device))
+    else:
+        _ext.call_cpu("cme_cpu_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n)
+    return out

@@ -1,0 +1,119 @@
+#!/usr/bin/env python3
+"""Single-GPU benchmarks for the BASELINE.md headline primitives. One JSON line
+per measurement with the reference number it is compared against.
+
+  copy       1 GiB 16-B copy (achievable-HBM calibration)
+  scan       2^26 elements: look-back / Blelloch / Hillis-Steele (BASELINE #11)
+  reduce     2^26 elements
+  spmvscan   the 15 final-project shapes (BASELINE #19-21, synthetic values)
+  cipher     19.76 MB moby-dick x16 (BASELINE #1-3)
+  pagerank   2^21 nodes, avg 8 edges, 20 iterations (BASELINE #5)
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=10, warmup=2):
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import cme213x
+    from cme213x.ops import elementwise, scan as sc
+
+    want = lambda k: args.only is None or k in args.only  # noqa: E731
+    dev = torch.device("cuda")
+
+    if want("copy"):
+        a = torch.empty(1 << 28, dtype=torch.float32, device=dev).uniform_()
+        b = torch.empty_like(a)
+        ms = timeit(lambda: elementwise.copy_(b, a))
+        emit(bench="copy", bytes=2 * a.numel() * 4, ms=ms, GBps=2 * a.numel() * 4 / ms / 1e6)
+        ms = timeit(lambda: b.copy_(a))
+        emit(bench="copy_torch", bytes=2 * a.numel() * 4, ms=ms, GBps=2 * a.numel() * 4 / ms / 1e6)
+        del a, b
+
+    if want("scan"):
+        n = 1 << 26
+        x = torch.rand(n, device=dev)
+        y = torch.empty_like(x)
+        for algo in ("lookback", "blelloch", "hillis"):
+            ms = timeit(lambda: sc.scan(x, True, y, algo))
+            emit(bench="scan", algo=algo, n=n, ms=ms, GBps=8 * n / ms / 1e6, ref_ms=15.85,
+                 speedup_vs_ref=15.85 / ms)
+        ms = timeit(lambda: torch.cumsum(x, 0, out=y))
+        emit(bench="scan", algo="torch.cumsum", n=n, ms=ms, GBps=8 * n / ms / 1e6)
+        xi = torch.randint(0, 100, (n,), device=dev, dtype=torch.int32)
+        yi = torch.empty_like(xi)
+        ms = timeit(lambda: sc.scan(xi, True, yi))
+        emit(bench="scan", algo="lookback-int32", n=n, ms=ms, GBps=8 * n / ms / 1e6)
+        for algo in ("vector", "tree"):
+            ms = timeit(lambda: sc.reduce(x, "sum", algo))
+            emit(bench="reduce", algo=algo, n=n, ms=ms, GBps=4 * n / ms / 1e6)
+        ms = timeit(lambda: x.sum())
+        emit(bench="reduce", algo="torch.sum", n=n, ms=ms, GBps=4 * n / ms / 1e6)
+        del x, y, xi, yi
+
+    if want("spmvscan"):
+        from cme213x.models.spmv_scan import BENCH_SHAPES, REF_MS, SpmvScanSolver, generate
+
+        for name, (n, p, N) in BENCH_SHAPES.items():
+            prob = generate(n, p, 100000, N, seed=1)
+            sol = SpmvScanSolver(prob, dev)
+            sol.run(2)
+            ms = timeit(lambda: sol.run(), iters=5, warmup=1)
+            emit(bench="spmvscan", matrix=name, n=n, p=p, N=N, ms=ms, GBps=12 * n * N / ms / 1e6,
+                 ref_ms=REF_MS[name], speedup_vs_ref=REF_MS[name] / ms)
+
+    if want("cipher"):
+        path = "/root/reference/hw/hw1/programming/mobydick.txt"
+        text = np.fromfile(path, dtype=np.uint8) if os.path.exists(path) else \
+            np.random.default_rng(0).integers(0, 128, 1235150, dtype=np.uint8)
+        for copies in (16, 208):
+            d = torch.from_numpy(np.tile(text, copies)).to(dev)
+            o = torch.empty_like(d)
+            for w in ("char", "uint", "uint2", "uint4"):
+                ms = timeit(lambda: elementwise.shift_cipher(d, 3, o, width=w))
+                emit(bench="cipher", width=w, bytes=d.numel(), ms=ms, GBps_rw=2 * d.numel() / ms / 1e6)
+
+    if want("pagerank"):
+        from cme213x.ops.graph import bytes_model, iterate, make_graph
+
+        g = make_graph(1 << 21, 8).to(dev)
+        x0 = torch.full((1 << 21,), 1.0 / (1 << 21), device=dev)
+        for grp in (1, 4, 8, 16):
+            ms = timeit(lambda: iterate(g, x0, 20, grp))
+            emit(bench="pagerank", group=grp, ms=ms, GBps_model=bytes_model(g, 20) / ms / 1e6, ref_ms=1188.11,
+                 speedup_vs_ref=1188.11 / ms)
+
+
+if __name__ == "__main__":
+    main()

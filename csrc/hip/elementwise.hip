@@ -77,6 +77,45 @@ __global__ __launch_bounds__(256) void copy_u128_kernel(const u32x4* __restrict_
     for (; i < n; i += stride) out[i] = in[i];
 }
 
+// Copy-rate calibration space: UNROLL x {nt, plain} x grid size.
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void copy_tune_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                        size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if constexpr (NT) v[u] = __builtin_nontemporal_load(&in[i + u * stride]);
+            else v[u] = in[i + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if constexpr (NT) __builtin_nontemporal_store(v[u], &out[i + u * stride]);
+            else out[i + u * stride] = v[u];
+        }
+    }
+    for (; i < n; i += stride) out[i] = in[i];
+}
+
+// Block-contiguous copy: each block streams one contiguous chunk (no grid stride).
+template <int UNROLL>
+__global__ __launch_bounds__(256) void copy_chunk_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                         size_t n, size_t per_block) {
+    size_t b0 = blockIdx.x * per_block;
+    size_t b1 = b0 + per_block < n ? b0 + per_block : n;
+    for (size_t i = b0 + threadIdx.x; i < b1; i += 256 * UNROLL) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            if (i + u * 256 < b1) v[u] = in[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            if (i + u * 256 < b1) out[i + u * 256] = v[u];
+    }
+}
+
 // a[i] *= b[i] (float), 16 B per lane.
 __global__ __launch_bounds__(256) void mul_f32_kernel(float* __restrict__ a, const float* __restrict__ b, size_t n4,
                                                       size_t n) {
@@ -147,5 +186,30 @@ CME_EXPORT int cme_mul_f32(float* a, const float* b, long long n, void* stream) 
     size_t n4 = (size_t)n / 4;
     hipLaunchKernelGGL(mul_f32_kernel, dim3(stream_grid(n4 ? n4 : 1, 256)), dim3(256), 0, as_stream(stream), a, b,
                        n4, (size_t)n);
+    CME_LAUNCH_STATUS();
+}
+
+// mode 0: grid-stride (unroll 1/2/4/8, nt 0/1, blocks/CU); mode 1: chunked.
+CME_EXPORT int cme_copy_tune(const void* in, void* out, long long nbytes, int mode, int unroll, int nt,
+                             int blocks_per_cu, void* stream) {
+    hipStream_t s = as_stream(stream);
+    size_t m = (size_t)nbytes / 16;
+    const u32x4* a = (const u32x4*)in;
+    u32x4* b = (u32x4*)out;
+    unsigned grid = (unsigned)(256 * blocks_per_cu);
+    if (mode == 1) {
+        size_t per = (m + grid - 1) / grid;
+        hipLaunchKernelGGL(copy_chunk_kernel<4>, dim3(grid), dim3(256), 0, s, a, b, m, per);
+        CME_LAUNCH_STATUS();
+    }
+#define CT(U, N) hipLaunchKernelGGL((copy_tune_kernel<U, N>), dim3(grid), dim3(256), 0, s, a, b, m)
+    if (nt) {
+        switch (unroll) { case 1: CT(1, true); break; case 2: CT(2, true); break; case 4: CT(4, true); break;
+                          default: CT(8, true); }
+    } else {
+        switch (unroll) { case 1: CT(1, false); break; case 2: CT(2, false); break; case 4: CT(4, false); break;
+                          default: CT(8, false); }
+    }
+#undef CT
     CME_LAUNCH_STATUS();
 }

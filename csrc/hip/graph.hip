@@ -15,6 +15,9 @@
 #include "cme213/common.h"
 #include "cme213/wave.h"
 
+// Keep a*b+c as two roundings, like the CPU oracle (bitwise parity).
+#pragma clang fp contract(off)
+
 namespace {
 
 __global__ __launch_bounds__(256) void prescale_kernel(const float* __restrict__ x, const float* __restrict__ inv,

@@ -1,0 +1,561 @@
+// Scan and reduction family (Lecture16 / Harris scan.pdf / nvr-2008-003,
+// Lecture05 tree reduction), written for wave64.
+//
+//  * cme_scan           single-pass decoupled look-back scan (the fast one):
+//                       4096-element tiles, 16 B/lane coalesced loads, DPP wave
+//                       scans, one 8-B granule per tile for the hand-off.
+//  * cme_scan_mlevel    multi-level scan-then-add (Harris Fig. 5) with a
+//                       selectable block algorithm: Blelloch work-efficient
+//                       up/down-sweep in LDS with bank-conflict-free padding, or
+//                       Hillis-Steele (naive, O(n log n)).
+//  * cme_reduce         two-pass block reduction (grid-stride 16-B loads, DPP
+//                       wave reduce, LDS across waves) and the lecture's
+//                       shared-memory tree (`s = blockDim/2; s >>= 1`) variant.
+//  * cme_segscan        single-pass segmented inclusive scan with head flags.
+//  * cme_spmv_scan_step fused final-project step: a[i] *= xx[i] then inclusive
+//                       segmented scan of a (segment heads as a bitmask).
+#include "cme213/common.h"
+#include "cme213/lookback.h"
+#include "cme213/wave.h"
+
+using namespace cme;
+
+namespace {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanWaves = kScanThreads / kWave;
+constexpr int kScanItemsPerLane = 16;  // 4 x 16-B vectors
+constexpr int kScanTile = kScanThreads * kScanItemsPerLane;  // 4096
+
+template <typename T>
+struct Vec4 {
+    T x, y, z, w;
+};
+
+template <typename T>
+__device__ __forceinline__ Vec4<T> load_v4(const T* p, long long i, long long n, T id) {
+    Vec4<T> r;
+    if (i + 3 < n) {
+        typedef T v4 __attribute__((ext_vector_type(4)));
+        v4 v = *reinterpret_cast<const v4*>(p + i);
+        r.x = v.x;
+        r.y = v.y;
+        r.z = v.z;
+        r.w = v.w;
+    } else {
+        r.x = i < n ? p[i] : id;
+        r.y = i + 1 < n ? p[i + 1] : id;
+        r.z = i + 2 < n ? p[i + 2] : id;
+        r.w = i + 3 < n ? p[i + 3] : id;
+    }
+    return r;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_v4(T* p, long long i, long long n, const Vec4<T>& r) {
+    if (i + 3 < n) {
+        typedef T v4 __attribute__((ext_vector_type(4)));
+        v4 v = {r.x, r.y, r.z, r.w};
+        *reinterpret_cast<v4*>(p + i) = v;
+    } else {
+        if (i < n) p[i] = r.x;
+        if (i + 1 < n) p[i + 1] = r.y;
+        if (i + 2 < n) p[i + 2] = r.z;
+        if (i + 3 < n) p[i + 3] = r.w;
+    }
+}
+
+// ------------------------------------------------------------ look-back scan
+template <typename T, bool EXCLUSIVE>
+__global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                                     long long n, uint64_t* desc, unsigned* counter,
+                                                                     unsigned* timeout) {
+    __shared__ int s_tile;
+    __shared__ T s_wtot[kScanWaves];
+    __shared__ T s_prefix;
+    const int tile = lb_ticket(counter, &s_tile);
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const long long base = (long long)tile * kScanTile + wid * (kWave * 16);
+
+    Vec4<T> v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = load_v4(in, base + k * 256 + lane * 4, n, T(0));
+
+    // in-lane inclusive scan of each 4-vector, wave scans of the lane totals,
+    // serial carry across the 4 wave-rows
+    T run = T(0);
+    T ex[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        T a = v[k].x, b = a + v[k].y, c = b + v[k].z, d = c + v[k].w;
+        T wt;
+        T e = wave_exclusive_scan<OpAdd>(d, &wt);
+        ex[k] = run + e;
+        run = run + wt;
+        if (EXCLUSIVE) {
+            v[k].w = c;
+            v[k].z = b;
+            v[k].y = a;
+            v[k].x = T(0);
+        } else {
+            v[k].y = b;
+            v[k].z = c;
+            v[k].w = d;
+        }
+    }
+    if (lane == 0) s_wtot[wid] = run;
+    __syncthreads();
+    T wpre = T(0), tot = T(0);
+#pragma unroll
+    for (int w = 0; w < kScanWaves; ++w) {
+        T t = s_wtot[w];
+        if (w < wid) wpre = wpre + t;
+        tot = tot + t;
+    }
+    if (wid == 0) {
+        if (tile == 0) {
+            if (lane == 0) {
+                lb_publish(desc, kStInclusive, lb_bits(tot));
+                s_prefix = T(0);
+            }
+        } else {
+            if (lane == 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
+            T pre = lb_lookback<T, false>(desc, tile, timeout);
+            if (lane == 0) {
+                lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
+                s_prefix = pre;
+            }
+        }
+    }
+    __syncthreads();
+    const T p = s_prefix + wpre;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const T q = p + ex[k];
+        Vec4<T> r{q + v[k].x, q + v[k].y, q + v[k].z, q + v[k].w};
+        store_v4(out, base + k * 256 + lane * 4, n, r);
+    }
+}
+
+// ------------------------------------------------------------ multi-level
+// Block algorithms operate on 2*kMLThreads elements in LDS.
+constexpr int kMLThreads = 256;
+constexpr int kMLElems = 2 * kMLThreads;
+// ds_read/write_b32 bank of byte address a is (a/4) % 32 on gfx950: pad one
+// word every 32 (Harris' CONFLICT_FREE_OFFSET with LOG_NUM_BANKS = 5).
+__host__ __device__ constexpr int cf(int i) { return i + (i >> 5); }
+
+template <typename T>
+__device__ void blelloch_block(T* s, T& total) {
+    const int t = threadIdx.x;
+    int offset = 1;
+    for (int d = kMLElems >> 1; d > 0; d >>= 1) {  // up-sweep (reduce)
+        __syncthreads();
+        if (t < d) {
+            int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+            s[cf(bi)] += s[cf(ai)];
+        }
+        offset <<= 1;
+    }
+    __syncthreads();
+    total = s[cf(kMLElems - 1)];
+    __syncthreads();
+    if (t == 0) s[cf(kMLElems - 1)] = T(0);
+    for (int d = 1; d < kMLElems; d <<= 1) {  // down-sweep
+        offset >>= 1;
+        __syncthreads();
+        if (t < d) {
+            int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+            T x = s[cf(ai)];
+            s[cf(ai)] = s[cf(bi)];
+            s[cf(bi)] += x;
+        }
+    }
+    __syncthreads();
+}
+
+// Hillis-Steele inclusive scan (double-buffered), then shift to exclusive.
+template <typename T>
+__device__ void hillis_block(T* s, T* s2, T& total) {
+    const int t = threadIdx.x;
+    T* src = s;
+    T* dst = s2;
+    for (int off = 1; off < kMLElems; off <<= 1) {
+        __syncthreads();
+        for (int i = t; i < kMLElems; i += kMLThreads) dst[cf(i)] = i >= off ? src[cf(i)] + src[cf(i - off)] : src[cf(i)];
+        T* tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    __syncthreads();
+    total = src[cf(kMLElems - 1)];
+    for (int i = t; i < kMLElems; i += kMLThreads) dst[cf(i)] = i ? src[cf(i - 1)] : T(0);
+    __syncthreads();
+    if (dst != s)
+        for (int i = t; i < kMLElems; i += kMLThreads) s[cf(i)] = dst[cf(i)];
+    __syncthreads();
+}
+
+template <typename T, int ALGO>
+__global__ __launch_bounds__(kMLThreads) void scan_block_kernel(const T* in, T* out, T* sums, long long n) {
+    __shared__ T s[cf(kMLElems) + 1];
+    __shared__ T s2[ALGO == 1 ? cf(kMLElems) + 1 : 1];
+    const long long b = (long long)blockIdx.x * kMLElems;
+    for (int i = threadIdx.x; i < kMLElems; i += kMLThreads) s[cf(i)] = b + i < n ? in[b + i] : T(0);
+    T total;
+    if constexpr (ALGO == 0) blelloch_block(s, total);
+    else hillis_block(s, s2, total);
+    for (int i = threadIdx.x; i < kMLElems; i += kMLThreads)
+        if (b + i < n) out[b + i] = s[cf(i)];
+    if (threadIdx.x == 0 && sums) sums[blockIdx.x] = total;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void add_offsets_kernel(T* __restrict__ out, const T* __restrict__ offs, long long n) {
+    const long long b = (long long)blockIdx.x * kMLElems;
+    const T o = offs[blockIdx.x];
+    for (int i = threadIdx.x; i < kMLElems; i += 256)
+        if (b + i < n) out[b + i] += o;
+}
+
+template <typename T>
+__global__ void to_inclusive_kernel(const T* __restrict__ in, T* __restrict__ out, long long n) {
+    long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i < n) out[i] += in[i];
+}
+
+// ------------------------------------------------------------ reduction
+template <typename T, typename Op>
+__global__ __launch_bounds__(256) void reduce_partial_kernel(const T* __restrict__ in, long long n, T* __restrict__ part,
+                                                             Op op) {
+    __shared__ T lds[4];
+    T acc = Op::template identity<T>();
+    const long long stride = (long long)gridDim.x * 256 * 4;
+    for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+        Vec4<T> v = load_v4(in, i, n, Op::template identity<T>());
+        acc = op(acc, op(op(v.x, v.y), op(v.z, v.w)));
+    }
+    T r = block_reduce<4>(acc, lds, op);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+template <typename T, typename Op>
+__global__ __launch_bounds__(1024) void reduce_final_kernel(const T* __restrict__ part, int m, T* __restrict__ out,
+                                                            Op op) {
+    __shared__ T lds[16];
+    T acc = Op::template identity<T>();
+    for (int i = threadIdx.x; i < m; i += 1024) acc = op(acc, part[i]);
+    T r = block_reduce<16>(acc, lds, op);
+    if (threadIdx.x == 0) *out = r;
+}
+
+// The lecture's shared-memory tree (Lecture05 slides 15-16), one element per
+// thread per step; kept for the optimisation ladder.
+template <typename T>
+__global__ __launch_bounds__(256) void reduce_tree_kernel(const T* __restrict__ in, long long n, T* __restrict__ part) {
+    __shared__ T s[256];
+    T acc = T(0);
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) acc += in[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) s[threadIdx.x] += s[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
+// ------------------------------------------------------------ segmented scan
+// Pair operator for (flag, value): (f1,v1) . (f2,v2) = (f1|f2, f2 ? v2 : v1+v2)
+__device__ __forceinline__ void seg_combine(uint32_t& f, float& v, uint32_t fs, float vs) {
+    v = f ? v : vs + v;
+    f = f | fs;
+}
+
+// Wave inclusive segmented scan via DPP (flags 0/1 per lane).
+__device__ __forceinline__ float wave_segscan(float v, uint32_t f, uint32_t* f_out) {
+#define SEG_STEP(CTRL, RM)                                           \
+    {                                                                \
+        float vs = dpp_move<CTRL, RM>(0.0f, v);                      \
+        uint32_t fs = dpp_move<CTRL, RM>(0u, f);                     \
+        seg_combine(f, v, fs, vs);                                   \
+    }
+    SEG_STEP(kDppRowShr1, 0xf)
+    SEG_STEP(kDppRowShr2, 0xf)
+    SEG_STEP(kDppRowShr4, 0xf)
+    SEG_STEP(kDppRowShr8, 0xf)
+    SEG_STEP(kDppRowBcast15, 0xa)
+    SEG_STEP(kDppRowBcast31, 0xc)
+#undef SEG_STEP
+    *f_out = f;
+    return v;
+}
+
+// flags source: MODE 0 = uint8 per element, MODE 1 = bitmask words (bit i%32
+// of word i/32). FUSED_MUL: v = a[i]*x[i] before scanning (final project).
+template <int MODE, bool FUSED_MUL>
+__global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
+                                                               float* __restrict__ out, const void* __restrict__ flags,
+                                                               long long n, uint64_t* desc, unsigned* counter,
+                                                               unsigned* timeout) {
+    __shared__ int s_tile;
+    __shared__ float s_wv[kScanWaves];
+    __shared__ uint32_t s_wf[kScanWaves];
+    __shared__ float s_prefix;
+    const int tile = lb_ticket(counter, &s_tile);
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const long long base = (long long)tile * kScanTile + wid * (kWave * 16);
+
+    float val[4][4];
+    uint32_t fl[4][4];
+    float run_v = 0.f;   // running (segment-aware) value across the 4 rows
+    uint32_t run_f = 0;  // any head seen so far in this wave
+    float ex_v[4];
+    uint32_t ex_f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const long long i = base + k * 256 + lane * 4;
+        Vec4<float> a = load_v4(in, i, n, 0.f);
+        if constexpr (FUSED_MUL) {
+            Vec4<float> x = load_v4(xmul, i, n, 0.f);
+            a.x *= x.x;
+            a.y *= x.y;
+            a.z *= x.z;
+            a.w *= x.w;
+        }
+        uint32_t f4;
+        if constexpr (MODE == 0) {
+            const uint8_t* fp = (const uint8_t*)flags;
+            if (i + 3 < n) {
+                f4 = *reinterpret_cast<const uint32_t*>(fp + i);
+                f4 = (f4 & 1u) | ((f4 >> 7) & 2u) | ((f4 >> 14) & 4u) | ((f4 >> 21) & 8u);
+            } else {
+                f4 = 0;
+                for (int j = 0; j < 4; ++j)
+                    if (i + j < n && fp[i + j]) f4 |= 1u << j;
+            }
+        } else {
+            const uint32_t* fw = (const uint32_t*)flags;
+            f4 = i < n ? (fw[i >> 5] >> (i & 31)) & 0xfu : 0u;
+        }
+        // in-lane inclusive segmented scan of 4 values
+        float v0 = a.x, v1 = a.y, v2 = a.z, v3 = a.w;
+        uint32_t g0 = f4 & 1, g1 = (f4 >> 1) & 1, g2 = (f4 >> 2) & 1, g3 = (f4 >> 3) & 1;
+        v1 = g1 ? v1 : v0 + v1;
+        v2 = g2 ? v2 : v1 + v2;
+        v3 = g3 ? v3 : v2 + v3;
+        val[k][0] = v0;
+        val[k][1] = v1;
+        val[k][2] = v2;
+        val[k][3] = v3;
+        fl[k][0] = g0;
+        fl[k][1] = g0 | g1;
+        fl[k][2] = g0 | g1 | g2;
+        fl[k][3] = g0 | g1 | g2 | g3;
+        // wave scan of lane totals (value v3, flag = any head in lane)
+        uint32_t lf;
+        float inc = wave_segscan(v3, fl[k][3], &lf);
+        // exclusive (shift by one lane); lane 0 gets the carry from earlier rows
+        float e_v = dpp_move<kDppWaveShr1>(0.f, inc);
+        uint32_t e_f = dpp_move<kDppWaveShr1>(0u, lf);
+        float row_tot_v = wave_readlane(inc, kWave - 1);
+        uint32_t row_tot_f = (uint32_t)__builtin_amdgcn_readlane((int)lf, kWave - 1);
+        // combine carry (run) with the exclusive lane prefix: carry applies
+        // unless a head occurred in earlier lanes of this row
+        ex_v[k] = e_f ? e_v : run_v + e_v;
+        ex_f[k] = e_f | run_f;
+        run_v = row_tot_f ? row_tot_v : run_v + row_tot_v;
+        run_f = run_f | row_tot_f;
+    }
+    if (lane == 0) {
+        s_wv[wid] = run_v;
+        s_wf[wid] = run_f;
+    }
+    __syncthreads();
+    // wave prefix (segment-aware) and tile aggregate
+    float wpre_v = 0.f;
+    uint32_t wpre_f = 0;
+    float tot_v = 0.f;
+    uint32_t tot_f = 0;
+#pragma unroll
+    for (int w = 0; w < kScanWaves; ++w) {
+        const float tv = s_wv[w];
+        const uint32_t tf = s_wf[w];
+        if (w < wid) {
+            wpre_v = tf ? tv : wpre_v + tv;
+            wpre_f |= tf;
+        }
+        tot_v = tf ? tv : tot_v + tv;
+        tot_f |= tf;
+    }
+    if (wid == 0) {
+        const uint32_t hf = tot_f ? kStFlag : 0u;
+        if (tile == 0) {
+            if (lane == 0) {
+                lb_publish(desc, kStInclusive | hf, __builtin_bit_cast(uint32_t, tot_v));
+                s_prefix = 0.f;
+            }
+        } else {
+            if (lane == 0) lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v));
+            float pre = lb_lookback<float, true>(desc, tile, timeout);
+            if (lane == 0) {
+                float incl = tot_f ? tot_v : pre + tot_v;
+                lb_publish(desc + tile, kStInclusive | hf, __builtin_bit_cast(uint32_t, incl));
+                s_prefix = pre;
+            }
+        }
+    }
+    __syncthreads();
+    // carry into this wave: tile prefix unless a head precedes in the tile
+    const float tile_pre = s_prefix;
+    const float wcarry = wpre_f ? wpre_v : tile_pre + wpre_v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float c = ex_f[k] ? ex_v[k] : wcarry + ex_v[k];
+        Vec4<float> r;
+        r.x = fl[k][0] ? val[k][0] : c + val[k][0];
+        r.y = fl[k][1] ? val[k][1] : c + val[k][1];
+        r.z = fl[k][2] ? val[k][2] : c + val[k][2];
+        r.w = fl[k][3] ? val[k][3] : c + val[k][3];
+        store_v4(out, base + k * 256 + lane * 4, n, r);
+    }
+}
+
+template <typename T>
+int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
+    if (n <= 0) return 0;
+    const int tiles = (int)((n + kScanTile - 1) / kScanTile);
+    uint64_t* desc = (uint64_t*)ws;
+    unsigned* counter = (unsigned*)(desc + tiles);
+    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    if (exclusive)
+        hipLaunchKernelGGL((scan_lookback_kernel<T, true>), dim3(tiles), dim3(kScanThreads), 0, s, in, out, n, desc,
+                           counter, counter + 1);
+    else
+        hipLaunchKernelGGL((scan_lookback_kernel<T, false>), dim3(tiles), dim3(kScanThreads), 0, s, in, out, n, desc,
+                           counter, counter + 1);
+    CME_LAUNCH_STATUS();
+}
+
+// Recursive scan-then-add; `ws` must hold sum(levels) elements (see
+// cme_scan_mlevel_ws_elems). Produces an EXCLUSIVE scan.
+template <typename T>
+int mlevel(const T* in, T* out, long long n, int algo, T* ws, hipStream_t s) {
+    const long long blocks = (n + kMLElems - 1) / kMLElems;
+    T* sums = blocks > 1 ? ws : nullptr;
+    if (algo == 0)
+        hipLaunchKernelGGL((scan_block_kernel<T, 0>), dim3((unsigned)blocks), dim3(kMLThreads), 0, s, in, out, sums, n);
+    else
+        hipLaunchKernelGGL((scan_block_kernel<T, 1>), dim3((unsigned)blocks), dim3(kMLThreads), 0, s, in, out, sums, n);
+    CME_TRY(hipGetLastError());
+    if (blocks > 1) {
+        int rc = mlevel<T>(sums, sums, blocks, algo, ws + blocks, s);
+        if (rc) return rc;
+        hipLaunchKernelGGL(add_offsets_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, out, sums, n);
+        CME_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace
+
+// dtype: 0 f32, 1 i32, 2 u32. ws: >= 8*ceil(n/4096) + 16 bytes.
+CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream) {
+    hipStream_t s = as_stream(stream);
+    switch (dtype) {
+        case 0: return launch_scan<float>((const float*)in, (float*)out, n, exclusive, ws, s);
+        case 1: return launch_scan<int>((const int*)in, (int*)out, n, exclusive, ws, s);
+        case 2: return launch_scan<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, exclusive, ws, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1) / kScanTile) * 8 + 16; }
+
+CME_EXPORT long long cme_scan_mlevel_ws_elems(long long n) {
+    long long tot = 0;
+    long long b = (n + kMLElems - 1) / kMLElems;
+    while (b > 1) {
+        tot += b;
+        b = (b + kMLElems - 1) / kMLElems;
+    }
+    return tot + 1;
+}
+
+// algo: 0 Blelloch, 1 Hillis-Steele; dtype 0 f32, 1 i32. inclusive via add-back.
+CME_EXPORT int cme_scan_mlevel(const void* in, void* out, long long n, int dtype, int algo, int exclusive, void* ws,
+                               void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 0) return 0;
+    int rc;
+    if (dtype == 0) rc = mlevel<float>((const float*)in, (float*)out, n, algo, (float*)ws, s);
+    else if (dtype == 1) rc = mlevel<int>((const int*)in, (int*)out, n, algo, (int*)ws, s);
+    else return (int)hipErrorInvalidValue;
+    if (rc) return rc;
+    if (!exclusive) {
+        unsigned g = cdiv(n, 256);
+        if (dtype == 0) hipLaunchKernelGGL(to_inclusive_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, (float*)out, n);
+        else hipLaunchKernelGGL(to_inclusive_kernel<int>, dim3(g), dim3(256), 0, s, (const int*)in, (int*)out, n);
+    }
+    CME_LAUNCH_STATUS();
+}
+
+// op: 0 sum, 1 max, 2 min; dtype 0 f32, 1 i32. algo 0 = DPP/vector, 1 = LDS tree (sum only).
+// part: >= 2048 elements of scratch. result written to `out` (device).
+CME_EXPORT int cme_reduce(const void* in, long long n, int dtype, int op, int algo, void* part, void* out,
+                          void* stream) {
+    hipStream_t s = as_stream(stream);
+    const int grid = 1024;
+#define RED(T, OP)                                                                                              \
+    hipLaunchKernelGGL((reduce_partial_kernel<T, OP>), dim3(grid), dim3(256), 0, s, (const T*)in, n, (T*)part, OP()); \
+    hipLaunchKernelGGL((reduce_final_kernel<T, OP>), dim3(1), dim3(1024), 0, s, (const T*)part, grid, (T*)out, OP());
+    if (algo == 1) {
+        if (op != 0) return (int)hipErrorInvalidValue;
+        if (dtype == 0) {
+            hipLaunchKernelGGL(reduce_tree_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)in, n, (float*)part);
+            hipLaunchKernelGGL((reduce_final_kernel<float, OpAdd>), dim3(1), dim3(1024), 0, s, (const float*)part,
+                               grid, (float*)out, OpAdd());
+        } else {
+            hipLaunchKernelGGL(reduce_tree_kernel<int>, dim3(grid), dim3(256), 0, s, (const int*)in, n, (int*)part);
+            hipLaunchKernelGGL((reduce_final_kernel<int, OpAdd>), dim3(1), dim3(1024), 0, s, (const int*)part, grid,
+                               (int*)out, OpAdd());
+        }
+        CME_LAUNCH_STATUS();
+    }
+    if (dtype == 0) {
+        if (op == 0) { RED(float, OpAdd) }
+        else if (op == 1) { RED(float, OpMax) }
+        else { RED(float, OpMin) }
+    } else if (dtype == 1) {
+        if (op == 0) { RED(int, OpAdd) }
+        else if (op == 1) { RED(int, OpMax) }
+        else { RED(int, OpMin) }
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+#undef RED
+    CME_LAUNCH_STATUS();
+}
+
+// Segmented inclusive scan (float add). flag_mode 0: uint8 per element;
+// 1: bitmask words. xmul != null fuses in[i]*xmul[i] (final-project step).
+CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const void* flags, int flag_mode,
+                           long long n, void* ws, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 0) return 0;
+    const int tiles = (int)((n + kScanTile - 1) / kScanTile);
+    uint64_t* desc = (uint64_t*)ws;
+    unsigned* counter = (unsigned*)(desc + tiles);
+    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+#define SEG(M, F) \
+    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(tiles), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, counter, counter + 1)
+    if (flag_mode == 0) {
+        if (xmul) SEG(0, true); else SEG(0, false);
+    } else {
+        if (xmul) SEG(1, true); else SEG(1, false);
+    }
+#undef SEG
+    CME_LAUNCH_STATUS();
+}

@@ -1,0 +1,158 @@
+"""Scan / reduce / segmented scan vs numpy fp64 oracles; the final project's
+SpMV-scan against the reference checker's small fixture and the fp64
+serial algorithm."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cme213x.models.spmv_scan import (SpmvScanProblem, SpmvScanSolver, errors, generate, load,
+                                      reference_solution, run_fp, save)
+from cme213x.ops.scan import head_flags_from_offsets, reduce, scan, segmented_scan
+
+SMALL = "/root/reference/hw/hw_final/programming/aux/CheckOutput"
+
+
+def _np_segscan(v, heads):
+    out = np.empty_like(v, dtype=np.float64)
+    run = 0.0
+    for i, x in enumerate(v.astype(np.float64)):
+        run = x if (i == 0 or heads[i]) else run + x
+        out[i] = run
+    return out
+
+
+@pytest.mark.parametrize("exclusive", [False, True])
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
+def test_scan_cpu(exclusive, dtype):
+    x = torch.randint(-5, 6, (10007,), dtype=torch.int32).to(dtype)
+    y = scan(x, exclusive)
+    ref = np.cumsum(x.numpy().astype(np.float64))
+    if exclusive:
+        ref = np.concatenate([[0], ref[:-1]])
+    np.testing.assert_array_equal(y.numpy().astype(np.float64), ref)
+
+
+def test_reduce_cpu():
+    x = torch.arange(1000, dtype=torch.int32)
+    assert reduce(x).item() == 499500
+    assert reduce(x, "max").item() == 999
+    assert reduce(x, "min").item() == 0
+
+
+def test_segscan_cpu_and_flags():
+    rng = np.random.default_rng(1)
+    n = 5000
+    s = np.concatenate([[0], np.sort(rng.choice(np.arange(1, n), 300, replace=False)), [n]]).astype(np.int32)
+    heads = np.zeros(n, bool)
+    heads[s[:-1]] = True
+    v = rng.standard_normal(n).astype(np.float32)
+    ref = _np_segscan(v, heads)
+    for bitmask in (True, False):
+        f = head_flags_from_offsets(torch.from_numpy(s), n, bitmask=bitmask)
+        out = segmented_scan(torch.from_numpy(v), f)
+        np.testing.assert_allclose(out.numpy(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_small_fixture_matches_reference_output():
+    a_path, x_path = os.path.join(SMALL, "small_a.txt"), os.path.join(SMALL, "small_x.txt")
+    if not os.path.exists(a_path):
+        pytest.skip("reference fixture not mounted")
+    prob = load(a_path, x_path)
+    ref = reference_solution(prob)
+    b_ref = np.fromfile(os.path.join(SMALL, "small_b.txt"), sep=" ")
+    np.testing.assert_allclose(ref, b_ref, rtol=1e-6)  # small_b.txt is single precision on purpose
+    sol = SpmvScanSolver(prob, "cpu")
+    out = sol.run().numpy()
+    np.testing.assert_allclose(out, b_ref, rtol=1e-6)
+
+
+def test_generator_and_io_roundtrip(tmp_path):
+    prob = generate(2000, 150, 500, 3, seed=2)
+    prob.validate()
+    save(prob, str(tmp_path / "a.txt"), str(tmp_path / "x.txt"))
+    q = load(str(tmp_path / "a.txt"), str(tmp_path / "x.txt"))
+    assert q.iters == 3 and np.array_equal(q.s, prob.s) and np.array_equal(q.k, prob.k)
+    np.testing.assert_array_equal(q.a, prob.a)
+    os.chdir(tmp_path)
+    res = run_fp(str(tmp_path / "a.txt"), str(tmp_path / "x.txt"), cpu_check=True, device="cpu")
+    assert res["relL2"] < 1e-5
+    assert (tmp_path / "b.txt").exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 1 << 20, 3_000_001])
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_lookback_gpu(gpu, n, dtype, exclusive):
+    x = torch.randint(-3, 4, (n,), dtype=torch.int32).to(dtype)
+    ref = np.cumsum(x.numpy().astype(np.int64))
+    if exclusive:
+        ref = np.concatenate([[0], ref[:-1]])
+    y = scan(x.to(gpu), exclusive).cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(y, ref)  # small integers: exact in fp32 too
+
+
+@pytest.mark.gpu
+def test_scan_uint32_gpu(gpu):
+    x = torch.randint(0, 100, (1 << 18,), dtype=torch.int32)
+    y = scan(x.to(gpu).view(torch.uint32), exclusive=True).view(torch.int32).cpu()
+    ref = torch.cumsum(x.to(torch.int64), 0) - x
+    assert torch.equal(y.to(torch.int64), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["blelloch", "hillis"])
+@pytest.mark.parametrize("n", [5, 512, 513, 262145, 1 << 20])
+def test_scan_mlevel_gpu(gpu, algo, n):
+    x = torch.randint(-3, 4, (n,), dtype=torch.int32)
+    for excl in (True, False):
+        ref = np.cumsum(x.numpy().astype(np.int64))
+        if excl:
+            ref = np.concatenate([[0], ref[:-1]])
+        y = scan(x.to(gpu), excl, algo=algo).cpu().numpy()
+        np.testing.assert_array_equal(y, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("op", ["sum", "max", "min"])
+@pytest.mark.parametrize("algo", ["vector", "tree"])
+def test_reduce_gpu(gpu, op, algo):
+    if algo == "tree" and op != "sum":
+        pytest.skip("tree variant is sum-only")
+    x = torch.randint(-1000, 1000, (3_000_017,), dtype=torch.int32)
+    ref = {"sum": x.sum(), "max": x.max(), "min": x.min()}[op].item()
+    assert reduce(x.to(gpu), op, algo).item() == ref
+    xf = torch.randn(1_000_003)
+    r = reduce(xf.to(gpu), op, algo).item()
+    rf = {"sum": xf.double().sum(), "max": xf.max(), "min": xf.min()}[op].item()
+    assert abs(r - rf) <= 1e-3 * max(1.0, abs(rf))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nseg", [1, 7, 1000, 200000])
+@pytest.mark.parametrize("bitmask", [True, False])
+def test_segscan_gpu(gpu, nseg, bitmask):
+    rng = np.random.default_rng(nseg)
+    n = 1_000_003
+    s = np.concatenate([[0], np.sort(rng.choice(np.arange(1, n), nseg - 1, replace=False)), [n]]).astype(np.int32)
+    v = rng.integers(-4, 5, n).astype(np.float32)  # integers: exact sums
+    m = rng.integers(-2, 3, n).astype(np.float32)
+    heads = np.zeros(n, bool)
+    heads[s[:-1]] = True
+    ref = _np_segscan(v * m, heads)
+    f = head_flags_from_offsets(torch.from_numpy(s), n, gpu, bitmask)
+    out = segmented_scan(torch.from_numpy(v).to(gpu), f, mul=torch.from_numpy(m).to(gpu)).cpu().numpy()
+    np.testing.assert_array_equal(out.astype(np.float64), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(37035, 3128, 6), (3_105_536, 1_000_004, 3), (4_000_000, 1999, 3)])
+def test_spmv_scan_gpu_vs_fp64(gpu, shape):
+    n, p, N = shape
+    prob = generate(n, p, 10000, N, seed=5)
+    sol = SpmvScanSolver(prob, gpu)
+    b = sol.run().cpu().numpy()
+    e = errors(reference_solution(prob), b)
+    assert e["relL2"] < 1e-5, e
