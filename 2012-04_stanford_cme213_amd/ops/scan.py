@@ -21,7 +21,7 @@ from .. import _ext
 _ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_mlevel", "ppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_reduce", "pqiiippp")
-_ext.proto(_ext.HIP_PROTOS, "cme_segscan", "pppppiqpp")
+_ext.proto(_ext.HIP_PROTOS, "cme_segscan", "ppppiqpp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_scan", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_reduce", "pqiip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_segscan", "ppppiq")

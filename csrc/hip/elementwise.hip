@@ -62,21 +62,6 @@ __global__ __launch_bounds__(256) void shift_u128_kernel(const u32x4* __restrict
     for (; i < n; i += stride) out[i] = f(in[i]);
 }
 
-template <int UNROLL>
-__global__ __launch_bounds__(256) void copy_u128_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
-                                                        size_t n) {
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
-        u32x4 v[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(&in[i + u * stride]);
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) __builtin_nontemporal_store(v[u], &out[i + u * stride]);
-    }
-    for (; i < n; i += stride) out[i] = in[i];
-}
-
 // Copy-rate calibration space: UNROLL x {nt, plain} x grid size.
 template <int UNROLL, bool NT>
 __global__ __launch_bounds__(256) void copy_tune_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
@@ -173,8 +158,10 @@ CME_EXPORT int cme_shift_cipher(const uint8_t* in, uint8_t* out, long long n, in
 CME_EXPORT int cme_copy_bytes(const void* in, void* out, long long nbytes, void* stream) {
     hipStream_t s = as_stream(stream);
     size_t m = (size_t)nbytes / 16;
-    if (m) hipLaunchKernelGGL(copy_u128_kernel<4>, dim3(stream_grid(m, 256, 4)), dim3(256), 0, s, (const u32x4*)in,
-                              (u32x4*)out, m);
+    // measured best on MI355X (benchmarks/tune_copy.py): 1 vector per lane per
+    // iteration, non-temporal, 4 blocks of 256 per CU, grid-stride
+    if (m) hipLaunchKernelGGL((copy_tune_kernel<1, true>), dim3(stream_grid(m, 256, 4)), dim3(256), 0, s,
+                              (const u32x4*)in, (u32x4*)out, m);
     size_t body = m * 16;
     if ((size_t)nbytes > body)
         hipLaunchKernelGGL(shift_u8_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)in + body, (uint8_t*)out + body,

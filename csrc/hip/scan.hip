@@ -66,28 +66,36 @@ __device__ __forceinline__ void store_v4(T* p, long long i, long long n, const V
 }
 
 // ------------------------------------------------------------ look-back scan
-template <typename T, bool EXCLUSIVE>
+// ROWS 16-B vectors per lane (tile = 256 * 4 * ROWS elements). LOOKBACK=false
+// is a timing-only diagnostic arm (tiles scanned independently: wrong result).
+template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                                     long long n, uint64_t* desc, unsigned* counter,
+                                                                     long long n, uint64_t* desc, int tiles,
                                                                      unsigned* timeout) {
-    __shared__ int s_tile;
-    __shared__ T s_wtot[kScanWaves];
-    __shared__ T s_prefix;
-    const int tile = lb_ticket(counter, &s_tile);
+    constexpr int TILE = kScanThreads * 4 * ROWS;
+    constexpr int WAVE_ELEMS = kWave * 4 * ROWS;
+    __shared__ T s_wtot[2][kScanWaves];
+    __shared__ T s_prefix[2];
     const int lane = lane_id();
+    int parity = 0;
+    // Persistent: block b scans tiles b, b+G, b+2G, ... in order (G = grid size,
+    // at most 4 blocks of 256 per CU: co-resident), so every tile's
+    // predecessors are owned by running blocks -- no ordering ticket (a single
+    // atomic word saturates at ~88 ops/us) and no dispatch-order assumption.
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
     const int wid = threadIdx.x / kWave;
-    const long long base = (long long)tile * kScanTile + wid * (kWave * 16);
+    const long long base = (long long)tile * TILE + wid * WAVE_ELEMS;
 
-    Vec4<T> v[4];
+    Vec4<T> v[ROWS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = load_v4(in, base + k * 256 + lane * 4, n, T(0));
+    for (int k = 0; k < ROWS; ++k) v[k] = load_v4(in, base + k * 256 + lane * 4, n, T(0));
 
     // in-lane inclusive scan of each 4-vector, wave scans of the lane totals,
-    // serial carry across the 4 wave-rows
+    // serial carry across the wave-rows
     T run = T(0);
-    T ex[4];
+    T ex[ROWS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < ROWS; ++k) {
         T a = v[k].x, b = a + v[k].y, c = b + v[k].z, d = c + v[k].w;
         T wt;
         T e = wave_exclusive_scan<OpAdd>(d, &wt);
@@ -104,38 +112,41 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
             v[k].w = d;
         }
     }
-    if (lane == 0) s_wtot[wid] = run;
+    if (lane == 0) s_wtot[parity][wid] = run;
     __syncthreads();
     T wpre = T(0), tot = T(0);
 #pragma unroll
     for (int w = 0; w < kScanWaves; ++w) {
-        T t = s_wtot[w];
+        T t = s_wtot[parity][w];
         if (w < wid) wpre = wpre + t;
         tot = tot + t;
     }
-    if (wid == 0) {
+    if (!LOOKBACK) {
+        if (threadIdx.x == 0) s_prefix[parity] = T(0);
+    } else if (wid == 0) {
         if (tile == 0) {
             if (lane == 0) {
                 lb_publish(desc, kStInclusive, lb_bits(tot));
-                s_prefix = T(0);
+                s_prefix[parity] = T(0);
             }
         } else {
             if (lane == 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
             T pre = lb_lookback<T, false>(desc, tile, timeout);
             if (lane == 0) {
                 lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
-                s_prefix = pre;
+                s_prefix[parity] = pre;
             }
         }
     }
     __syncthreads();
-    const T p = s_prefix + wpre;
+    const T p = s_prefix[parity] + wpre;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < ROWS; ++k) {
         const T q = p + ex[k];
         Vec4<T> r{q + v[k].x, q + v[k].y, q + v[k].z, q + v[k].w};
         store_v4(out, base + k * 256 + lane * 4, n, r);
     }
+    }  // tile loop
 }
 
 // ------------------------------------------------------------ multi-level
@@ -297,14 +308,18 @@ __device__ __forceinline__ float wave_segscan(float v, uint32_t f, uint32_t* f_o
 template <int MODE, bool FUSED_MUL>
 __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
                                                                float* __restrict__ out, const void* __restrict__ flags,
-                                                               long long n, uint64_t* desc, unsigned* counter,
+                                                               long long n, uint64_t* desc, int tiles,
                                                                unsigned* timeout) {
-    __shared__ int s_tile;
-    __shared__ float s_wv[kScanWaves];
-    __shared__ uint32_t s_wf[kScanWaves];
-    __shared__ float s_prefix;
-    const int tile = lb_ticket(counter, &s_tile);
+    __shared__ float s_wv_[2][kScanWaves];
+    __shared__ uint32_t s_wf_[2][kScanWaves];
+    __shared__ float s_prefix_[2];
     const int lane = lane_id();
+    int parity = 0;
+    // persistent, co-resident grid (see scan_lookback_kernel)
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
+    float* s_wv = s_wv_[parity];
+    uint32_t* s_wf = s_wf_[parity];
+    float& s_prefix = s_prefix_[parity];
     const int wid = threadIdx.x / kWave;
     const long long base = (long long)tile * kScanTile + wid * (kWave * 16);
 
@@ -421,21 +436,26 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
         r.w = fl[k][3] ? val[k][3] : c + val[k][3];
         store_v4(out, base + k * 256 + lane * 4, n, r);
     }
+    }  // tile loop
 }
+
+// Co-resident persistent grid: <= 4 blocks of 256 threads per CU.
+constexpr int kPersistBlocks = 4 * kNumCU;
 
 template <typename T>
 int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
+    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
     uint64_t* desc = (uint64_t*)ws;
-    unsigned* counter = (unsigned*)(desc + tiles);
+    unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
     if (exclusive)
-        hipLaunchKernelGGL((scan_lookback_kernel<T, true>), dim3(tiles), dim3(kScanThreads), 0, s, in, out, n, desc,
-                           counter, counter + 1);
+        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kScanItemsPerLane / 4>), dim3(grid), dim3(kScanThreads), 0,
+                           s, in, out, n, desc, tiles, timeout);
     else
-        hipLaunchKernelGGL((scan_lookback_kernel<T, false>), dim3(tiles), dim3(kScanThreads), 0, s, in, out, n, desc,
-                           counter, counter + 1);
+        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kScanItemsPerLane / 4>), dim3(grid), dim3(kScanThreads), 0,
+                           s, in, out, n, desc, tiles, timeout);
     CME_LAUNCH_STATUS();
 }
 
@@ -473,6 +493,29 @@ CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int e
 }
 
 CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1) / kScanTile) * 8 + 16; }
+
+// Diagnostic/tuning arms of the look-back scan (f32 exclusive): rows = 4/8/16
+// vectors per lane, lookback = 0 skips the cross-tile pass (wrong results;
+// isolates the hand-off cost).
+CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows, int lookback, void* ws,
+                             void* stream) {
+    hipStream_t s = as_stream(stream);
+    const long long tile = 1024LL * rows;
+    const int tiles = (int)((n + tile - 1) / tile);
+    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
+    uint64_t* desc = (uint64_t*)ws;
+    unsigned* timeout = (unsigned*)(desc + tiles);
+    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+#define ST(R, L)                                                                                                   \
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L>), dim3(grid), dim3(kScanThreads), 0, s, in, out, n,  \
+                       desc, tiles, timeout)
+    if (rows == 4) { if (lookback) ST(4, true); else ST(4, false); }
+    else if (rows == 8) { if (lookback) ST(8, true); else ST(8, false); }
+    else if (rows == 16) { if (lookback) ST(16, true); else ST(16, false); }
+    else return (int)hipErrorInvalidValue;
+#undef ST
+    CME_LAUNCH_STATUS();
+}
 
 CME_EXPORT long long cme_scan_mlevel_ws_elems(long long n) {
     long long tot = 0;
@@ -546,11 +589,12 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     hipStream_t s = as_stream(stream);
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
+    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
     uint64_t* desc = (uint64_t*)ws;
-    unsigned* counter = (unsigned*)(desc + tiles);
+    unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
 #define SEG(M, F) \
-    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(tiles), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, counter, counter + 1)
+    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, tiles, timeout)
     if (flag_mode == 0) {
         if (xmul) SEG(0, true); else SEG(0, false);
     } else {
