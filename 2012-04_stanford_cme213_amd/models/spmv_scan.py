@@ -25,7 +25,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
-from ..ops.scan import head_flags_from_offsets, segmented_scan
+from ..ops.scan import head_flags_from_offsets, segmented_scan, spmv_scan_run
 from ..utils.gridio import write_vector
 from ..utils.timer import EventTimer
 
@@ -129,9 +129,7 @@ class SpmvScanSolver:
         segmented_scan(self.a, self.flags, out=self.a, mul=self.xx)
 
     def run(self, iters: int | None = None) -> torch.Tensor:
-        for _ in range(self.prob.iters if iters is None else iters):
-            self.step()
-        return self.a
+        return spmv_scan_run(self.a, self.xx, self.flags, self.prob.iters if iters is None else iters)
 
 
 def reference_solution(prob: SpmvScanProblem, iters: int | None = None) -> np.ndarray:

@@ -19,9 +19,11 @@ import torch
 from .. import _ext
 
 _ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_scan_rts", "ppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_mlevel", "ppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_reduce", "pqiiippp")
 _ext.proto(_ext.HIP_PROTOS, "cme_segscan", "ppppiqpp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_run", "pppqipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_scan", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_reduce", "pqiip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_segscan", "ppppiq")
@@ -50,9 +52,10 @@ def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
 
 
 def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
-         algo: str = "lookback") -> torch.Tensor:
+         algo: str = "rts") -> torch.Tensor:
     """Prefix sum of a 1-D contiguous float32/int32/uint32 tensor.
-    algo: "lookback" (single pass), "blelloch" or "hillis" (multi-level)."""
+    algo: "lookback" (single pass), "rts" (reduce-then-scan, deterministic),
+    "blelloch" or "hillis" (multi-level scan-then-add)."""
     if not x.is_contiguous():
         x = x.contiguous()
     out = torch.empty_like(x) if out is None else out
@@ -62,6 +65,9 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
         if algo == "lookback":
             _ext.call_hip("cme_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           _lookback_ws(x).data_ptr(), s)
+        elif algo == "rts":
+            _ext.call_hip("cme_scan_rts", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
+                          workspace(x.device, 8192, "rts").data_ptr(), s)
         else:
             if out.data_ptr() == x.data_ptr() and not exclusive:
                 raise ValueError("in-place inclusive multi-level scan is not supported")
@@ -121,3 +127,16 @@ def segmented_scan(x: torch.Tensor, flags: torch.Tensor, out: torch.Tensor | Non
     else:
         _ext.call_cpu("cme_cpu_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n)
     return out
+
+
+def spmv_scan_run(a: torch.Tensor, xx: torch.Tensor, flags: torch.Tensor, iters: int) -> torch.Tensor:
+    """``iters`` in-place steps ``a <- segscan(a * xx)`` (bitmask heads): one
+    descriptor memset + one kernel per step, no host synchronisation."""
+    if not a.is_cuda:
+        for _ in range(iters):
+            segmented_scan(a, flags, out=a, mul=xx)
+        return a
+    assert flags.dtype == torch.int32, "bitmask flags expected"
+    _ext.call_hip("cme_spmv_scan_run", a.data_ptr(), xx.data_ptr(), flags.data_ptr(), a.numel(), iters,
+                  _lookback_ws(a).data_ptr(), _ext.stream_ptr(a.device))
+    return a

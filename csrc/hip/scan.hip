@@ -149,6 +149,120 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     }  // tile loop
 }
 
+// ------------------------------------------------------------ reduce-then-scan
+// Deterministic three-kernel scan (no inter-workgroup hand-off inside a
+// launch): K1 reduces contiguous chunks, K2 scans the chunk totals in one
+// block, K3 rescans each chunk tile by tile with the carry in LDS, prefetching
+// the next tile while the current one is scanned. 12 B/element of traffic,
+// bitwise reproducible (fixed summation tree).
+constexpr int kRtsBlocks = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(256) void rts_reduce_kernel(const T* __restrict__ in, long long n, long long chunk,
+                                                         T* __restrict__ part) {
+    __shared__ T lds[4];
+    const long long b0 = (long long)blockIdx.x * chunk;
+    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    T acc = T(0);
+    for (long long i = b0 + threadIdx.x * 4; i < b1; i += 1024) {
+        Vec4<T> v = load_v4(in, i, b1, T(0));
+        acc = acc + ((v.x + v.y) + (v.z + v.w));
+    }
+    T r = block_reduce<4>(acc, lds, OpAdd());
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void rts_partials_kernel(T* part, int m) {
+    __shared__ T lds[16];
+    T carry = T(0);
+    for (int base = 0; base < m; base += 1024) {
+        const int i = base + threadIdx.x;
+        T v = i < m ? part[i] : T(0);
+        T tot;
+        T ex = block_exclusive_scan<16>(v, lds, tot, OpAdd());
+        if (i < m) part[i] = carry + ex;
+        carry = carry + tot;
+    }
+}
+
+template <typename T, bool EXCLUSIVE>
+__global__ __launch_bounds__(256) void rts_scan_kernel(const T* __restrict__ in, T* __restrict__ out, long long n,
+                                                       long long chunk, const T* __restrict__ part) {
+    __shared__ T s_wtot[2][kScanWaves];
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const long long b0 = (long long)blockIdx.x * chunk;
+    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    T carry = part[blockIdx.x];
+    Vec4<T> v[4], nv[4];
+    auto load_tile = [&](long long t0, Vec4<T>* dst) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = load_v4(in, t0 + wid * 1024 + k * 256 + lane * 4, b1, T(0));
+    };
+    if (b0 < b1) load_tile(b0, v);
+    int parity = 0;
+    for (long long t0 = b0; t0 < b1; t0 += kScanTile, parity ^= 1) {
+        if (t0 + kScanTile < b1) load_tile(t0 + kScanTile, nv);
+        T run = T(0);
+        T ex[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            T a = v[k].x, b = a + v[k].y, c = b + v[k].z, d = c + v[k].w;
+            T wt;
+            T e = wave_exclusive_scan<OpAdd>(d, &wt);
+            ex[k] = run + e;
+            run = run + wt;
+            if (EXCLUSIVE) {
+                v[k].w = c;
+                v[k].z = b;
+                v[k].y = a;
+                v[k].x = T(0);
+            } else {
+                v[k].y = b;
+                v[k].z = c;
+                v[k].w = d;
+            }
+        }
+        if (lane == 0) s_wtot[parity][wid] = run;
+        __syncthreads();
+        T wpre = T(0), tot = T(0);
+#pragma unroll
+        for (int w = 0; w < kScanWaves; ++w) {
+            T t = s_wtot[parity][w];
+            if (w < wid) wpre = wpre + t;
+            tot = tot + t;
+        }
+        const T p = carry + wpre;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const T q = p + ex[k];
+            Vec4<T> r{q + v[k].x, q + v[k].y, q + v[k].z, q + v[k].w};
+            store_v4(out, t0 + wid * 1024 + k * 256 + lane * 4, b1, r);
+        }
+        carry = carry + tot;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = nv[k];
+    }
+}
+
+template <typename T>
+int launch_rts(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
+    if (n <= 0) return 0;
+    long long tiles = (n + kScanTile - 1) / kScanTile;
+    int blocks = tiles < kRtsBlocks ? (int)tiles : kRtsBlocks;
+    long long chunk = ((tiles + blocks - 1) / blocks) * kScanTile;
+    blocks = (int)((n + chunk - 1) / chunk);
+    T* part = (T*)ws;
+    hipLaunchKernelGGL(rts_reduce_kernel<T>, dim3(blocks), dim3(256), 0, s, in, n, chunk, part);
+    hipLaunchKernelGGL(rts_partials_kernel<T>, dim3(1), dim3(1024), 0, s, part, blocks);
+    if (exclusive)
+        hipLaunchKernelGGL((rts_scan_kernel<T, true>), dim3(blocks), dim3(256), 0, s, in, out, n, chunk, part);
+    else
+        hipLaunchKernelGGL((rts_scan_kernel<T, false>), dim3(blocks), dim3(256), 0, s, in, out, n, chunk, part);
+    CME_LAUNCH_STATUS();
+}
+
 // ------------------------------------------------------------ multi-level
 // Block algorithms operate on 2*kMLThreads elements in LDS.
 constexpr int kMLThreads = 256;
@@ -309,7 +423,7 @@ template <int MODE, bool FUSED_MUL>
 __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
                                                                float* __restrict__ out, const void* __restrict__ flags,
                                                                long long n, uint64_t* desc, int tiles,
-                                                               unsigned* timeout) {
+                                                               unsigned* timeout, uint32_t epoch) {
     __shared__ float s_wv_[2][kScanWaves];
     __shared__ uint32_t s_wf_[2][kScanWaves];
     __shared__ float s_prefix_[2];
@@ -409,15 +523,15 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
         const uint32_t hf = tot_f ? kStFlag : 0u;
         if (tile == 0) {
             if (lane == 0) {
-                lb_publish(desc, kStInclusive | hf, __builtin_bit_cast(uint32_t, tot_v));
+                lb_publish(desc, kStInclusive | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
                 s_prefix = 0.f;
             }
         } else {
-            if (lane == 0) lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v));
-            float pre = lb_lookback<float, true>(desc, tile, timeout);
+            if (lane == 0) lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
+            float pre = lb_lookback<float, true>(desc, tile, timeout, epoch);
             if (lane == 0) {
                 float incl = tot_f ? tot_v : pre + tot_v;
-                lb_publish(desc + tile, kStInclusive | hf, __builtin_bit_cast(uint32_t, incl));
+                lb_publish(desc + tile, kStInclusive | hf, __builtin_bit_cast(uint32_t, incl), epoch);
                 s_prefix = pre;
             }
         }
@@ -439,14 +553,14 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     }  // tile loop
 }
 
-// Co-resident persistent grid: <= 4 blocks of 256 threads per CU.
-constexpr int kPersistBlocks = 4 * kNumCU;
-
 template <typename T>
 int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
-    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
+    static int bpc_e = persistent_blocks_per_cu(scan_lookback_kernel<T, true, kScanItemsPerLane / 4>, kScanThreads);
+    static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kScanItemsPerLane / 4>, kScanThreads);
+    const int cap = kNumCU * (exclusive ? bpc_e : bpc_i);
+    const int grid = tiles < cap ? tiles : cap;
     uint64_t* desc = (uint64_t*)ws;
     unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
@@ -481,6 +595,17 @@ int mlevel(const T* in, T* out, long long n, int algo, T* ws, hipStream_t s) {
 
 }  // namespace
 
+// Reduce-then-scan (deterministic). ws: >= 4 * 1024 bytes.
+CME_EXPORT int cme_scan_rts(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream) {
+    hipStream_t s = as_stream(stream);
+    switch (dtype) {
+        case 0: return launch_rts<float>((const float*)in, (float*)out, n, exclusive, ws, s);
+        case 1: return launch_rts<int>((const int*)in, (int*)out, n, exclusive, ws, s);
+        case 2: return launch_rts<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, exclusive, ws, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
 // dtype: 0 f32, 1 i32, 2 u32. ws: >= 8*ceil(n/4096) + 16 bytes.
 CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -502,7 +627,11 @@ CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows,
     hipStream_t s = as_stream(stream);
     const long long tile = 1024LL * rows;
     const int tiles = (int)((n + tile - 1) / tile);
-    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
+    int bpc = 1;
+    if (rows == 4) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 4, true>, kScanThreads);
+    else if (rows == 8) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 8, true>, kScanThreads);
+    else bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 16, true>, kScanThreads);
+    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
     uint64_t* desc = (uint64_t*)ws;
     unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
@@ -589,17 +718,36 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     hipStream_t s = as_stream(stream);
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
-    const int grid = tiles < kPersistBlocks ? tiles : kPersistBlocks;
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
+    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
     uint64_t* desc = (uint64_t*)ws;
     unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
 #define SEG(M, F) \
-    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, tiles, timeout)
+    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, tiles, timeout, 1u)
     if (flag_mode == 0) {
         if (xmul) SEG(0, true); else SEG(0, false);
     } else {
         if (xmul) SEG(1, true); else SEG(1, false);
     }
 #undef SEG
+    CME_LAUNCH_STATUS();
+}
+
+// Final-project driver: `iters` fused steps a <- segscan(a * xx) (bitmask
+// heads) with ONE descriptor memset; iteration i uses look-back epoch i+1.
+CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
+                                 void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 0 || iters <= 0) return 0;
+    const int tiles = (int)((n + kScanTile - 1) / kScanTile);
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
+    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
+    uint64_t* desc = (uint64_t*)ws;
+    unsigned* timeout = (unsigned*)(desc + tiles);
+    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    for (int it = 0; it < iters; ++it)
+        hipLaunchKernelGGL((segscan_kernel<1, true>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a, flags, n, desc,
+                           tiles, timeout, (uint32_t)(it + 1));
     CME_LAUNCH_STATUS();
 }

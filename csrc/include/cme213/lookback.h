@@ -19,11 +19,15 @@
 
 namespace cme {
 
+// Status word = (epoch << 8) | bits. A descriptor is valid for a launch only
+// when its epoch matches, so a multi-iteration driver zeroes the array ONCE
+// and gives iteration i epoch i+1 (epoch 0 never matches a zeroed word).
 enum : uint32_t { kStInvalid = 0, kStAggregate = 1, kStInclusive = 2, kStFlag = 4 };
 constexpr unsigned kSpinLimit = 1u << 22;
 
-__device__ __forceinline__ void lb_publish(uint64_t* d, uint32_t status, uint32_t vbits) {
-    __hip_atomic_store(d, ((uint64_t)status << 32) | vbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void lb_publish(uint64_t* d, uint32_t status, uint32_t vbits, uint32_t epoch = 0) {
+    __hip_atomic_store(d, ((uint64_t)((epoch << 8) | status) << 32) | vbits, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ uint64_t lb_poll(uint64_t* d) {
@@ -53,37 +57,60 @@ __device__ __forceinline__ T lb_val(uint64_t d) {
 // segmented scan the running value at the predecessor's end). `segmented`:
 // a predecessor whose status carries kStFlag terminates the walk (a segment
 // head lies inside it), like an inclusive one.
-template <typename T, bool SEGMENTED>
-__device__ T lb_lookback(uint64_t* desc, int tile, unsigned* timeout) {
+//
+// Each lane inspects D consecutive predecessors per poll (window 64*D); only
+// predecessors nearer than the first terminating one must be valid. Measured
+// on MI355X (benchmarks/tune_scan.py): D = 1 is fastest -- wider windows
+// multiply the memory-side poll traffic of spinning waves.
+template <typename T, bool SEGMENTED, int D = 1>
+__device__ T lb_lookback(uint64_t* desc, int tile, unsigned* timeout, uint32_t epoch = 0) {
     const int lane = lane_id();
     T prefix = T(0);
     int base = tile - 1;
     unsigned spins = 0;
     while (true) {
-        const int idx = base - lane;
-        uint64_t d;
-        uint32_t st;
+        uint64_t d[D];
+        T lsum;
+        bool lterm, lvalid;
         while (true) {
-            d = idx >= 0 ? lb_poll(desc + idx) : ((uint64_t)kStInclusive << 32);
-            st = (uint32_t)(d >> 32);
-            if (!__any(st == kStInvalid)) break;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const int idx = base - lane * D - j;
+                d[j] = idx >= 0 ? lb_poll(desc + idx) : ((uint64_t)((epoch << 8) | kStInclusive) << 32);
+            }
+            // per lane: nearest-first fold up to (and including) the first terminator
+            lsum = T(0);
+            lterm = false;
+            lvalid = true;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const uint32_t hi = (uint32_t)(d[j] >> 32);
+                const uint32_t st = (hi >> 8) == epoch ? (hi & 0xffu) : kStInvalid;
+                if (st == kStInvalid) d[j] = 0;
+                if (!lterm) {
+                    lvalid = lvalid && (st != kStInvalid);
+                    lsum = lsum + lb_val<T>(d[j]);
+                    lterm = (st & kStInclusive) || (SEGMENTED && (st & kStFlag));
+                }
+            }
+            const uint64_t tmask = __ballot(lterm);
+            const int k = tmask ? __builtin_ctzll(tmask) : kWave;  // nearest terminating lane
+            const bool need = lane <= k;
+            if (!__any(need && !lvalid)) break;
             if (++spins > kSpinLimit) {
                 if (lane == 0) atomicOr(timeout, 1u);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        const bool term = (st & kStInclusive) || (SEGMENTED && (st & kStFlag));
-        const uint64_t mask = __ballot(term);
-        T v = lb_val<T>(d);
-        if (mask) {
-            const int k = __builtin_ctzll(mask);
-            v = lane <= k ? v : T(0);
-            prefix = prefix + wave_reduce(v);
+        const uint64_t tmask = __ballot(lterm);
+        if (tmask) {
+            const int k = __builtin_ctzll(tmask);
+            prefix = prefix + wave_reduce(lane <= k ? lsum : T(0));
             return prefix;
         }
-        prefix = prefix + wave_reduce(v);
-        base -= kWave;
+        prefix = prefix + wave_reduce(lsum);
+        base -= kWave * D;
     }
 }
 

@@ -82,15 +82,16 @@ def test_generator_and_io_roundtrip(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 1 << 20, 3_000_001])
+@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 1 << 20, 3_000_001, 9_000_011])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
 @pytest.mark.parametrize("exclusive", [False, True])
-def test_scan_lookback_gpu(gpu, n, dtype, exclusive):
+@pytest.mark.parametrize("algo", ["lookback", "rts"])
+def test_scan_single_pass_gpu(gpu, n, dtype, exclusive, algo):
     x = torch.randint(-3, 4, (n,), dtype=torch.int32).to(dtype)
     ref = np.cumsum(x.numpy().astype(np.int64))
     if exclusive:
         ref = np.concatenate([[0], ref[:-1]])
-    y = scan(x.to(gpu), exclusive).cpu().numpy().astype(np.int64)
+    y = scan(x.to(gpu), exclusive, algo=algo).cpu().numpy().astype(np.int64)
     np.testing.assert_array_equal(y, ref)  # small integers: exact in fp32 too
 
 
