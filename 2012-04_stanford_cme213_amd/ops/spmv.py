@@ -1,0 +1,265 @@
+"""Sparse matrices and SpMV in the Bell & Garland formats (CSR-scalar,
+CSR-vector, ELL, DIA, COO, HYB), plus the structured-Laplacian generators
+(3/5/7/9/27-point) used in their evaluation (``refs/Bell SC 2009.pdf`` §4.2;
+``slides/Lecture22.pdf``).
+
+Conversions run once on the host (numpy, vectorised); the matrices then live
+on the device and every multiply is one HIP kernel (two for HYB).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _ext
+
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr", "ipppppifp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_ell", "iippppfp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_dia", "iiippppfp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_coo", "iqpppppfip")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
+
+
+# ---------------------------------------------------------------- formats
+@dataclass
+class CSR:
+    nrows: int
+    ncols: int
+    rp: torch.Tensor  # int32 [nrows+1]
+    col: torch.Tensor  # int32 [nnz]
+    val: torch.Tensor  # float32 [nnz]
+
+    @property
+    def nnz(self) -> int:
+        return self.col.numel()
+
+    def to(self, device) -> "CSR":
+        return CSR(self.nrows, self.ncols, self.rp.to(device), self.col.to(device), self.val.to(device))
+
+    def to_dense(self) -> torch.Tensor:
+        rows = torch.repeat_interleave(torch.arange(self.nrows), torch.diff(self.rp.cpu().long()))
+        d = torch.zeros(self.nrows, self.ncols)
+        d.index_put_((rows, self.col.cpu().long()), self.val.cpu(), accumulate=True)
+        return d
+
+
+@dataclass
+class ELL:
+    nrows: int
+    ncols: int
+    K: int
+    col: torch.Tensor  # int32 [K*nrows], column-major, -1 = padding
+    val: torch.Tensor  # float32 [K*nrows]
+
+    def to(self, device) -> "ELL":
+        return ELL(self.nrows, self.ncols, self.K, self.col.to(device), self.val.to(device))
+
+
+@dataclass
+class DIA:
+    nrows: int
+    ncols: int
+    offsets: torch.Tensor  # int32 [ndiag]
+    data: torch.Tensor  # float32 [ndiag*nrows], data[d*nrows + r] = A[r, r+off[d]]
+
+    def to(self, device) -> "DIA":
+        return DIA(self.nrows, self.ncols, self.offsets.to(device), self.data.to(device))
+
+
+@dataclass
+class COO:
+    nrows: int
+    ncols: int
+    row: torch.Tensor  # int32 [nnz], sorted
+    col: torch.Tensor
+    val: torch.Tensor
+
+    @property
+    def nnz(self) -> int:
+        return self.row.numel()
+
+    def to(self, device) -> "COO":
+        return COO(self.nrows, self.ncols, self.row.to(device), self.col.to(device), self.val.to(device))
+
+
+@dataclass
+class HYB:
+    ell: ELL
+    coo: COO
+
+    def to(self, device) -> "HYB":
+        return HYB(self.ell.to(device), self.coo.to(device))
+
+
+def csr_from_coo_arrays(nrows: int, ncols: int, r: np.ndarray, c: np.ndarray, v: np.ndarray) -> CSR:
+    order = np.lexsort((c, r))
+    r, c, v = r[order], c[order], v[order]
+    rp = np.zeros(nrows + 1, dtype=np.int64)
+    np.add.at(rp, r + 1, 1)
+    rp = np.cumsum(rp)
+    return CSR(nrows, ncols, torch.from_numpy(rp.astype(np.int32)), torch.from_numpy(c.astype(np.int32)),
+               torch.from_numpy(v.astype(np.float32)))
+
+
+def _row_ids(a: CSR) -> np.ndarray:
+    return np.repeat(np.arange(a.nrows, dtype=np.int64), np.diff(a.rp.cpu().numpy().astype(np.int64)))
+
+
+def to_coo(a: CSR) -> COO:
+    return COO(a.nrows, a.ncols, torch.from_numpy(_row_ids(a).astype(np.int32)), a.col.cpu().clone(),
+               a.val.cpu().clone())
+
+
+def to_ell(a: CSR, K: int | None = None) -> tuple[ELL, COO]:
+    """ELL with K columns (default: max row length); entries beyond K go to
+    the returned COO remainder (empty when K >= max row length)."""
+    rp = a.rp.cpu().numpy().astype(np.int64)
+    lens = np.diff(rp)
+    K = int(lens.max()) if K is None else int(K)
+    rows = _row_ids(a)
+    pos = np.arange(a.nnz, dtype=np.int64) - rp[rows]
+    col = a.col.cpu().numpy()
+    val = a.val.cpu().numpy()
+    keep = pos < K
+    ecol = np.full(K * a.nrows, -1, dtype=np.int32)
+    eval_ = np.zeros(K * a.nrows, dtype=np.float32)
+    idx = pos[keep] * a.nrows + rows[keep]
+    ecol[idx] = col[keep]
+    eval_[idx] = val[keep]
+    rest = ~keep
+    coo = COO(a.nrows, a.ncols, torch.from_numpy(rows[rest].astype(np.int32)),
+              torch.from_numpy(col[rest].copy()), torch.from_numpy(val[rest].copy()))
+    return ELL(a.nrows, a.ncols, K, torch.from_numpy(ecol), torch.from_numpy(eval_)), coo
+
+
+def hyb_k(a: CSR) -> int:
+    """Bell & Garland's ELL width: the largest K such that at least
+    max(4096, nrows/3) rows have >= K nonzeros."""
+    lens = np.diff(a.rp.cpu().numpy().astype(np.int64))
+    need = max(4096, a.nrows // 3)
+    hist = np.bincount(lens)
+    rows_ge = np.cumsum(hist[::-1])[::-1]  # rows_ge[k] = #rows with len >= k
+    ks = np.nonzero(rows_ge >= need)[0]
+    return int(ks.max()) if ks.size else 0
+
+
+def to_hyb(a: CSR, K: int | None = None) -> HYB:
+    ell, coo = to_ell(a, hyb_k(a) if K is None else K)
+    return HYB(ell, coo)
+
+
+def to_dia(a: CSR, max_diags: int = 1024) -> DIA:
+    rows = _row_ids(a)
+    col = a.col.cpu().numpy().astype(np.int64)
+    off = col - rows
+    offs = np.unique(off)
+    if offs.size > max_diags:
+        raise ValueError(f"{offs.size} diagonals: DIA is not suitable for this matrix")
+    d_index = np.searchsorted(offs, off)
+    data = np.zeros(offs.size * a.nrows, dtype=np.float32)
+    np.add.at(data, d_index * a.nrows + rows, a.val.cpu().numpy())
+    return DIA(a.nrows, a.ncols, torch.from_numpy(offs.astype(np.int32)), torch.from_numpy(data))
+
+
+# ---------------------------------------------------------------- generators
+def laplacian(kind: str, n: int) -> CSR:
+    """Structured Laplacians on an n (1-D), n x n (2-D) or n^3 (3-D) grid:
+    "3pt", "5pt", "7pt", "9pt", "27pt" (Bell & Garland Table 2 family).
+    Diagonal = number of neighbours, off-diagonals -1."""
+    if kind == "3pt":
+        dims, stencil = (n,), [(-1,), (0,), (1,)]
+    elif kind == "5pt":
+        dims, stencil = (n, n), [(0, 0), (-1, 0), (1, 0), (0, -1), (0, 1)]
+    elif kind == "9pt":
+        dims, stencil = (n, n), [(i, j) for i in (-1, 0, 1) for j in (-1, 0, 1)]
+    elif kind == "7pt":
+        dims = (n, n, n)
+        stencil = [(0, 0, 0), (-1, 0, 0), (1, 0, 0), (0, -1, 0), (0, 1, 0), (0, 0, -1), (0, 0, 1)]
+    elif kind == "27pt":
+        dims = (n, n, n)
+        stencil = [(i, j, k) for i in (-1, 0, 1) for j in (-1, 0, 1) for k in (-1, 0, 1)]
+    else:
+        raise ValueError(kind)
+    N = int(np.prod(dims))
+    coords = np.stack(np.unravel_index(np.arange(N, dtype=np.int64), dims), axis=1)
+    rs, cs, vs = [], [], []
+    ncount = len(stencil) - 1
+    for off in stencil:
+        nb = coords + np.asarray(off)
+        ok = np.all((nb >= 0) & (nb < np.asarray(dims)), axis=1)
+        r = np.nonzero(ok)[0]
+        c = np.ravel_multi_index(tuple(nb[ok].T), dims)
+        rs.append(r)
+        cs.append(c)
+        vs.append(np.full(r.size, float(ncount) if not any(off) else -1.0, dtype=np.float32))
+    return csr_from_coo_arrays(N, N, np.concatenate(rs), np.concatenate(cs), np.concatenate(vs))
+
+
+def random_csr(nrows: int, ncols: int, avg_nnz: float, seed: int = 0, skew: bool = False) -> CSR:
+    """Random sparse matrix; ``skew`` draws power-law row lengths (the
+    unstructured corpus' load-imbalance case)."""
+    rng = np.random.default_rng(seed)
+    if skew:
+        lens = np.minimum((rng.pareto(1.5, nrows) + 1) * avg_nnz / 3, ncols).astype(np.int64)
+    else:
+        lens = rng.poisson(avg_nnz, nrows).astype(np.int64)
+    lens = np.maximum(lens, 1)
+    r = np.repeat(np.arange(nrows), lens)
+    c = rng.integers(0, ncols, r.size)
+    v = rng.uniform(-1, 1, r.size).astype(np.float32)
+    return csr_from_coo_arrays(nrows, ncols, r, c, v)
+
+
+# ---------------------------------------------------------------- multiply
+def auto_group(a: CSR) -> int:
+    """Lanes per row for CSR-vector: next power of two >= mean row length,
+    clamped to [2, 64]."""
+    mean = a.nnz / max(1, a.nrows)
+    g = 2
+    while g < mean and g < 64:
+        g *= 2
+    return g
+
+
+def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
+    """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
+    "scalar", "vector", or "auto" (vector with auto group)."""
+    if y is None:
+        nrows = a.ell.nrows if isinstance(a, HYB) else a.nrows
+        y = torch.zeros(nrows, dtype=torch.float32, device=x.device)
+    if not x.is_cuda:
+        if not isinstance(a, CSR):
+            raise TypeError("CPU path supports CSR only")
+        _ext.call_cpu("cme_cpu_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), float(beta))
+        return y
+    s = _ext.stream_ptr(x.device)
+    if isinstance(a, CSR):
+        g = 1 if kernel == "scalar" else auto_group(a)
+        _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
+                      y.data_ptr(), g, float(beta), s)
+    elif isinstance(a, ELL):
+        _ext.call_hip("cme_spmv_ell", a.nrows, a.K, a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(), y.data_ptr(),
+                      float(beta), s)
+    elif isinstance(a, DIA):
+        _ext.call_hip("cme_spmv_dia", a.nrows, a.ncols, a.offsets.numel(), a.offsets.data_ptr(), a.data.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), float(beta), s)
+    elif isinstance(a, COO):
+        _ext.call_hip("cme_spmv_coo", a.nrows, a.nnz, a.row.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), float(beta), 0, s)
+    elif isinstance(a, HYB):
+        spmv(a.ell, x, y, beta=beta)
+        if a.coo.nnz:
+            _ext.call_hip("cme_spmv_coo", a.coo.nrows, a.coo.nnz, a.coo.row.data_ptr(), a.coo.col.data_ptr(),
+                          a.coo.val.data_ptr(), x.data_ptr(), y.data_ptr(), 1.0, 1, s)
+    else:
+        raise TypeError(type(a))
+    return y
+
+
+def bytes_per_nnz(fmt: str) -> float:
+    """Bell & Garland's fp32 byte model per nonzero (their Table: DIA 4,
+    ELL 6... here value + index bytes): for GFLOP/s -> GB/s conversions."""
+    return {"dia": 4, "ell": 8, "csr": 8, "coo": 12, "hyb": 8}[fmt]

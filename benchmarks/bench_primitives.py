@@ -104,6 +104,12 @@ def main():
                 ms = timeit(lambda: elementwise.shift_cipher(d, 3, o, width=w))
                 emit(bench="cipher", width=w, bytes=d.numel(), ms=ms, GBps_rw=2 * d.numel() / ms / 1e6)
 
+    if want("transpose"):
+        bench_transpose(emit, timeit)
+
+    if want("spmv"):
+        bench_spmv(emit, timeit)
+
     if want("pagerank"):
         from cme213x.ops.graph import bytes_model, iterate, make_graph
 
@@ -113,6 +119,46 @@ def main():
             ms = timeit(lambda: iterate(g, x0, 20, grp))
             emit(bench="pagerank", group=grp, ms=ms, GBps_model=bytes_model(g, 20) / ms / 1e6, ref_ms=1188.11,
                  speedup_vs_ref=1188.11 / ms)
+
+
+def bench_transpose(emit, timeit):
+    import torch
+
+    from cme213x.ops.transpose import VARIANTS, transpose
+
+    ref = {8192: None, 4096: 130.0, 2048: 128.0}  # BASELINE #7/#8 best (LDS+pad+unroll, Fermi)
+    for n in (8192, 4096, 2048):
+        x = torch.rand(n, n, device="cuda")
+        out = torch.empty_like(x)
+        for v in VARIANTS:
+            ms = timeit(lambda: transpose(x, v, out))
+            gbps = 2 * n * n * 4 / ms / 1e6
+            emit(bench="transpose", n=n, variant=v, ms=ms, GBps=gbps, ref_GBps=ref[n],
+                 vs_ref=(gbps / ref[n]) if ref[n] else None)
+
+
+def bench_spmv(emit, timeit):
+    import torch
+
+    from cme213x.ops.spmv import laplacian, random_csr, spmv, to_coo, to_dia, to_ell, to_hyb
+
+    mats = {"5pt-1M": laplacian("5pt", 1000), "27pt-1M": laplacian("27pt", 100),
+            "random-1M": random_csr(1 << 20, 1 << 20, 16, seed=1), "skew-1M": random_csr(1 << 20, 1 << 20, 16,
+                                                                                             seed=2, skew=True)}
+    for name, a in mats.items():
+        x = torch.rand(a.ncols, device="cuda")
+        fmts = {"csr_scalar": a, "csr_vector": a, "ell": to_ell(a)[0], "coo": to_coo(a), "hyb": to_hyb(a)}
+        if name.startswith(("5pt", "27pt")):
+            fmts["dia"] = to_dia(a)
+        for f, m in fmts.items():
+            if f == "ell" and m.K > 64:
+                continue
+            md = m.to("cuda")
+            y = torch.empty(a.nrows, device="cuda")
+            kern = "scalar" if f == "csr_scalar" else "auto"
+            ms = timeit(lambda: spmv(md, x, y, kernel=kern), iters=20)
+            emit(bench="spmv", matrix=name, fmt=f, nnz=a.nnz, ms=ms, GFLOPs=2 * a.nnz / ms / 1e6,
+                 ref_GFLOPs={"5pt-1M": 39.6 if f == "dia" else None}.get(name))
 
 
 if __name__ == "__main__":

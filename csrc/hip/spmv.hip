@@ -1,0 +1,164 @@
+// Sparse matrix-vector multiply y = A x in the Bell & Garland formats
+// (refs/Bell SC 2009.pdf; slides/Lecture22.pdf; refs/Baskaran IBM 2009.pdf),
+// re-derived for wave64:
+//
+//  csr_scalar : one lane per row (CSR-scalar)
+//  csr_vector : G = 2..64 lanes per row, strided nnz, DPP/shuffle reduce
+//               (Baskaran's half-warp-per-row, generalised; G picked from the
+//               mean row length by the host)
+//  ell        : column-major padded ELLPACK (col < 0 = padding), lane per row,
+//               fully coalesced
+//  dia        : diagonal format, offsets + column-major diagonals, no column
+//               indices at all (structured Laplacians)
+//  coo        : flat segmented reduction: each wave takes 64*4 consecutive
+//               nonzeros, DPP segmented scan by row, one atomic add per
+//               (row segment x wave) -- load-balanced regardless of row lengths
+//  hyb        : ELL for the first K entries of each row + COO for the rest
+#include "cme213/common.h"
+#include "cme213/wave.h"
+
+using namespace cme;
+
+namespace {
+
+__global__ __launch_bounds__(256) void csr_scalar_kernel(int nrows, const int* __restrict__ rp,
+                                                         const int* __restrict__ col, const float* __restrict__ val,
+                                                         const float* __restrict__ x, float* __restrict__ y,
+                                                         float beta) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    float s = 0.f;
+    for (int j = rp[r]; j < rp[r + 1]; ++j) s += val[j] * x[col[j]];
+    y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void csr_vector_kernel(int nrows, const int* __restrict__ rp,
+                                                         const int* __restrict__ col, const float* __restrict__ val,
+                                                         const float* __restrict__ x, float* __restrict__ y,
+                                                         float beta) {
+    const int r = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    const int sub = threadIdx.x % G;
+    float s = 0.f;
+    if (r < nrows) {
+        const int b = rp[r], e = rp[r + 1];
+        for (int j = b + sub; j < e; j += G) s += val[j] * x[col[j]];
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (r < nrows && sub == 0) y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+__global__ __launch_bounds__(256) void ell_kernel(int nrows, int K, const int* __restrict__ col,
+                                                  const float* __restrict__ val, const float* __restrict__ x,
+                                                  float* __restrict__ y, float beta) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) {
+        const int c = col[(size_t)k * nrows + r];
+        if (c >= 0) s += val[(size_t)k * nrows + r] * x[c];
+    }
+    y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+__global__ __launch_bounds__(256) void dia_kernel(int nrows, int ncols, int ndiag, const int* __restrict__ offsets,
+                                                  const float* __restrict__ data, const float* __restrict__ x,
+                                                  float* __restrict__ y, float beta) {
+    __shared__ int s_off[64];
+    for (int i = threadIdx.x; i < ndiag && i < 64; i += blockDim.x) s_off[i] = offsets[i];
+    __syncthreads();
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    float s = 0.f;
+    for (int d = 0; d < ndiag; ++d) {
+        const int c = r + (d < 64 ? s_off[d] : offsets[d]);
+        if (c >= 0 && c < ncols) s += data[(size_t)d * nrows + r] * x[c];
+    }
+    y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+// COO: entries sorted by row. Each wave handles 256 consecutive entries as
+// 4 rounds of 64; segmented (by row) inclusive scan via DPP, lanes that end a
+// row segment (next lane has another row, or last lane) atomically add.
+__global__ __launch_bounds__(256) void coo_kernel(long long nnz, const int* __restrict__ row,
+                                                  const int* __restrict__ col, const float* __restrict__ val,
+                                                  const float* __restrict__ x, float* __restrict__ y) {
+    const int lane = lane_id();
+    const long long wave = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / kWave;
+    const long long base = wave * 256;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const long long i = base + k * 64 + lane;
+        const bool ok = i < nnz;
+        const int r = ok ? row[i] : -1;
+        float v = ok ? val[i] * x[col[i]] : 0.f;
+        // head flag: first lane or row differs from previous lane
+        const int rprev = dpp_move<kDppWaveShr1>(-2, r);
+        uint32_t f = (lane == 0 || rprev != r) ? 1u : 0u;
+#define SEG_STEP(CTRL, RM)                                 \
+    {                                                      \
+        float vs = dpp_move<CTRL, RM>(0.0f, v);            \
+        uint32_t fs = dpp_move<CTRL, RM>(0u, f);           \
+        v = f ? v : vs + v;                                \
+        f = f | fs;                                        \
+    }
+        SEG_STEP(kDppRowShr1, 0xf)
+        SEG_STEP(kDppRowShr2, 0xf)
+        SEG_STEP(kDppRowShr4, 0xf)
+        SEG_STEP(kDppRowShr8, 0xf)
+        SEG_STEP(kDppRowBcast15, 0xa)
+        SEG_STEP(kDppRowBcast31, 0xc)
+#undef SEG_STEP
+        const int rnext = dpp_move<kDppWaveShl1>(-3, r);
+        const bool tail = (lane == kWave - 1) || (rnext != r);
+        if (ok && tail) atomicAdd(&y[r], v);
+    }
+}
+
+__global__ void scale_kernel(float* y, int n, float beta) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = beta == 0.f ? 0.f : beta * y[i];
+}
+
+}  // namespace
+
+// y = A x (+ beta y). group: 1 scalar, else lanes per row (2..64).
+CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const float* val, const float* x, float* y,
+                            int group, float beta, void* stream) {
+    hipStream_t s = as_stream(stream);
+    switch (group) {
+        case 1: hipLaunchKernelGGL(csr_scalar_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+#define V(G) case G: hipLaunchKernelGGL(csr_vector_kernel<G>, dim3(cdiv((size_t)nrows * G, 256)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+        V(2) V(4) V(8) V(16) V(32) V(64)
+#undef V
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
+
+CME_EXPORT int cme_spmv_ell(int nrows, int K, const int* col, const float* val, const float* x, float* y, float beta,
+                            void* stream) {
+    hipLaunchKernelGGL(ell_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, as_stream(stream), nrows, K, col, val, x, y,
+                       beta);
+    CME_LAUNCH_STATUS();
+}
+
+CME_EXPORT int cme_spmv_dia(int nrows, int ncols, int ndiag, const int* offsets, const float* data, const float* x,
+                            float* y, float beta, void* stream) {
+    hipLaunchKernelGGL(dia_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, as_stream(stream), nrows, ncols, ndiag,
+                       offsets, data, x, y, beta);
+    CME_LAUNCH_STATUS();
+}
+
+// y = beta*y + A x for COO (beta applied first, then atomics accumulate).
+CME_EXPORT int cme_spmv_coo(int nrows, long long nnz, const int* row, const int* col, const float* val, const float* x,
+                            float* y, float beta, int accumulate, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (!accumulate) hipLaunchKernelGGL(scale_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, s, y, nrows, beta);
+    if (nnz > 0) {
+        const long long waves = (nnz + 255) / 256;
+        hipLaunchKernelGGL(coo_kernel, dim3(cdiv(waves * 64, 256)), dim3(256), 0, s, nnz, row, col, val, x, y);
+    }
+    CME_LAUNCH_STATUS();
+}

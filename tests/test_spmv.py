@@ -1,0 +1,66 @@
+"""SpMV formats vs dense / fp64 oracles; format conversions; generators."""
+import numpy as np
+import pytest
+import torch
+
+from cme213x.ops.spmv import (CSR, hyb_k, laplacian, random_csr, spmv, to_coo, to_dia, to_ell, to_hyb)
+
+
+def _ref(a: CSR, x):
+    rp = a.rp.numpy().astype(np.int64)
+    rows = np.repeat(np.arange(a.nrows), np.diff(rp))
+    y = np.zeros(a.nrows)
+    np.add.at(y, rows, a.val.numpy().astype(np.float64) * x.numpy().astype(np.float64)[a.col.numpy()])
+    return y
+
+
+@pytest.mark.parametrize("kind,n,deg", [("3pt", 50, 3), ("5pt", 20, 5), ("9pt", 12, 9), ("7pt", 6, 7), ("27pt", 5, 27)])
+def test_laplacian_structure(kind, n, deg):
+    a = laplacian(kind, n)
+    lens = np.diff(a.rp.numpy())
+    assert lens.max() == deg
+    d = a.to_dense()
+    assert torch.allclose(d, d.t())
+    assert torch.allclose(d.sum(1)[lens == deg], torch.zeros(int((lens == deg).sum())))
+
+
+def test_csr_cpu_and_conversions():
+    a = random_csr(500, 400, 7, seed=1)
+    x = torch.randn(400)
+    ref = _ref(a, x)
+    np.testing.assert_allclose(spmv(a, x).numpy(), ref, rtol=1e-4, atol=1e-4)
+    ell, rest = to_ell(a)
+    assert rest.nnz == 0 and ell.K == int(np.diff(a.rp.numpy()).max())
+    hyb = to_hyb(a)
+    assert hyb.ell.K == hyb_k(a)
+    assert to_coo(a).nnz == a.nnz
+    lap = laplacian("5pt", 10)
+    dia = to_dia(lap)
+    assert dia.offsets.tolist() == [-10, -1, 0, 1, 10]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "ell", "dia", "coo", "hyb"])
+def test_spmv_gpu(gpu, mat, fmt):
+    if mat == "5pt":
+        a = laplacian("5pt", 100)
+    elif mat == "27pt":
+        a = laplacian("27pt", 20)
+    elif mat == "random":
+        a = random_csr(20000, 15000, 12, seed=2)
+    else:
+        a = random_csr(20000, 20000, 20, seed=3, skew=True)
+    if fmt == "dia" and mat in ("random", "skew"):
+        pytest.skip("DIA only for structured matrices")
+    x = torch.randn(a.ncols)
+    ref = _ref(a, x)
+    dev = {"csr_scalar": a, "csr_vector": a, "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
+           "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
+    kernel = "scalar" if fmt == "csr_scalar" else "auto"
+    y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+    # beta accumulate
+    y0 = torch.randn(a.nrows, device=gpu)
+    y1 = spmv(dev, x.to(gpu), y0.clone(), kernel=kernel, beta=0.5).cpu().numpy()
+    np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
