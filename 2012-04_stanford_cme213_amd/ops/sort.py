@@ -1,0 +1,114 @@
+"""Sorting: GPU LSD radix sort (8-bit digits, stable, key-value), GPU
+merge-path merge sort, and the hw4 OpenMP radix / merge sorts.
+
+Keys: uint32 natively; int32 and float32 are mapped to order-preserving
+uint32 codes (sign-bit flip / IEEE total-order trick) and back.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+_ext.proto(_ext.HIP_PROTOS, "cme_radix_sort_u32", "ppppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_u32", "ppqii")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_serial_u32", "ppqi")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_merge_sort_i32", "ppqqqp")
+
+
+def _to_u32(k: torch.Tensor) -> torch.Tensor:
+    if k.dtype == torch.uint32:
+        return k.clone()
+    if k.dtype == torch.int32:
+        return (k.view(torch.int32) ^ torch.tensor(-(2 ** 31), dtype=torch.int32, device=k.device)).view(torch.uint32)
+    if k.dtype == torch.float32:
+        i = k.view(torch.int32)
+        mask = torch.where(i < 0, torch.tensor(-1, dtype=torch.int32, device=k.device),
+                           torch.tensor(-(2 ** 31), dtype=torch.int32, device=k.device))
+        return (i ^ mask).view(torch.uint32)
+    raise TypeError(f"unsupported key dtype {k.dtype}")
+
+
+def _from_u32(u: torch.Tensor, dtype) -> torch.Tensor:
+    if dtype == torch.uint32:
+        return u
+    i = u.view(torch.int32)
+    if dtype == torch.int32:
+        return i ^ torch.tensor(-(2 ** 31), dtype=torch.int32, device=u.device)
+    mask = torch.where(i >= 0, torch.tensor(-1, dtype=torch.int32, device=u.device),
+                       torch.tensor(-(2 ** 31), dtype=torch.int32, device=u.device))
+    return (i ^ mask).view(torch.float32)
+
+
+_ws: dict = {}
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    t = _ws.get(dev.index)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _ws[dev.index] = t
+    return t
+
+
+def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "radix", num_bits: int = 8):
+    """Sort a 1-D tensor (optionally carrying int32/uint32/float32 values).
+    GPU algos: "radix" (stable), "merge". CPU algos: "radix" (OpenMP,
+    ``num_bits`` per pass), "radix_serial", "merge" (OpenMP tasks, keys only).
+    Returns sorted keys (and values)."""
+    if keys.dim() != 1:
+        raise ValueError("1-D keys expected")
+    n = keys.numel()
+    dtype = keys.dtype
+    if keys.is_cuda:
+        k = _to_u32(keys.contiguous())
+        k2 = torch.empty_like(k)
+        v = v2 = None
+        if values is not None:
+            v = values.contiguous().clone().view(torch.uint32) if values.dtype != torch.uint32 else values.clone()
+            v2 = torch.empty_like(v)
+        s = _ext.stream_ptr(keys.device)
+        vp = v.data_ptr() if v is not None else None
+        v2p = v2.data_ptr() if v2 is not None else None
+        if algo == "radix":
+            ws = _workspace(keys.device, 2 * 1024 * 256 * 4 + 65536)
+            _ext.call_hip("cme_radix_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, 0, 32, ws.data_ptr(), s)
+        elif algo == "merge":
+            _ext.call_hip("cme_merge_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, s)
+        else:
+            raise ValueError(algo)
+        out = _from_u32(k, dtype)
+        if values is not None:
+            return out, v.view(values.dtype)
+        return out
+    if values is not None:
+        raise NotImplementedError("CPU key-value sort: use the GPU path")
+    if algo == "merge":
+        if dtype != torch.int32:
+            raise TypeError("CPU merge sort takes int32 keys (the hw4 driver's type)")
+        a = keys.clone()
+        tmp = torch.empty_like(a)
+        st = torch.zeros(1, dtype=torch.int32)
+        _ext.call_cpu("cme_cpu_merge_sort_i32", a.data_ptr(), tmp.data_ptr(), n, 2048, 2048, st.data_ptr())
+        return a if st.item() == 1 else tmp
+    k = _to_u32(keys.contiguous())
+    tmp = torch.empty_like(k)
+    if algo == "radix":
+        _ext.call_cpu("cme_cpu_radix_sort_u32", k.data_ptr(), tmp.data_ptr(), n, num_bits, 0)
+    elif algo == "radix_serial":
+        _ext.call_cpu("cme_cpu_radix_sort_serial_u32", k.data_ptr(), tmp.data_ptr(), n, num_bits)
+    else:
+        raise ValueError(algo)
+    return _from_u32(k, dtype)
+
+
+def merge_sort_cpu(keys: torch.Tensor, sort_threshold: int, merge_threshold: int) -> tuple[torch.Tensor, int]:
+    """The hw4 driver's merge sort with explicit thresholds; returns (sorted,
+    status) where status 1/-1 says which ping-pong buffer held the result."""
+    a = keys.clone()
+    tmp = torch.empty_like(a)
+    st = torch.zeros(1, dtype=torch.int32)
+    _ext.call_cpu("cme_cpu_merge_sort_i32", a.data_ptr(), tmp.data_ptr(), a.numel(), sort_threshold,
+                  merge_threshold, st.data_ptr())
+    return (a if st.item() == 1 else tmp), int(st.item())

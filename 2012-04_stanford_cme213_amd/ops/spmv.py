@@ -112,12 +112,14 @@ def to_coo(a: CSR) -> COO:
                a.val.cpu().clone())
 
 
-def to_ell(a: CSR, K: int | None = None) -> tuple[ELL, COO]:
+def to_ell(a: CSR, K: int | None = None, max_entries: int = 1 << 27) -> tuple[ELL, COO]:
     """ELL with K columns (default: max row length); entries beyond K go to
     the returned COO remainder (empty when K >= max row length)."""
     rp = a.rp.cpu().numpy().astype(np.int64)
     lens = np.diff(rp)
     K = int(lens.max()) if K is None else int(K)
+    if K * a.nrows > max_entries:
+        raise ValueError(f"ELL width {K} x {a.nrows} rows exceeds {max_entries} entries: use HYB")
     rows = _row_ids(a)
     pos = np.arange(a.nnz, dtype=np.int64) - rp[rows]
     col = a.col.cpu().numpy()

@@ -1,0 +1,331 @@
+// GPU sorting: LSD radix sort (8-bit digits) and merge-path merge sort.
+//
+// Parity: the hw4 OpenMP radix sort (hw/hw4/programming/radixsort.cpp:22-121:
+// per-block histograms -> reduce -> exclusive scan -> push-down offsets ->
+// per-block scatter) and merge sort (mergesort.cpp:31-144: recursive sort +
+// parallel merge split at the median via upper_bound), moved to wave64.
+//
+// Radix pass (reduce-then-scan structure -- no in-launch hand-offs):
+//   K1 upsweep  : block b histograms its contiguous chunk (LDS atomics) into
+//                 counts[digit * nblocks + b]
+//   K2 scan     : exclusive scan of counts (digit-major) -> global offsets
+//   K3 downsweep: block b re-reads its chunk tile by tile (4096 keys); keys are
+//                 ranked stably inside each wave with 8 ballots per item
+//                 (wave64 "match"), waves are combined per digit in LDS, the
+//                 tile is reordered by digit in LDS and written out so that
+//                 consecutive lanes store consecutive addresses of a digit run.
+//                 A running per-digit base in LDS carries the chunk across tiles.
+#include "cme213/common.h"
+#include "cme213/wave.h"
+
+using namespace cme;
+
+namespace {
+
+constexpr int kRadixBits = 8;
+constexpr int kBins = 1 << kRadixBits;
+constexpr int kSortThreads = 256;
+constexpr int kSortWaves = kSortThreads / kWave;
+constexpr int kItems = 16;  // keys per lane per tile
+constexpr int kSortTile = kSortThreads * kItems;  // 4096
+
+__device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift) { return (k >> shift) & (kBins - 1); }
+
+__global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint32_t* __restrict__ keys, long long n,
+                                                                     long long chunk, int shift, int nblocks,
+                                                                     uint32_t* __restrict__ counts) {
+    __shared__ uint32_t hist[kBins];
+    for (int i = threadIdx.x; i < kBins; i += kSortThreads) hist[i] = 0;
+    __syncthreads();
+    const long long b0 = (long long)blockIdx.x * chunk;
+    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    for (long long i = b0 + threadIdx.x * 4; i < b1; i += kSortThreads * 4) {
+        if (i + 3 < b1) {
+            const uint4 v = *reinterpret_cast<const uint4*>(keys + i);
+            atomicAdd(&hist[digit_of(v.x, shift)], 1u);
+            atomicAdd(&hist[digit_of(v.y, shift)], 1u);
+            atomicAdd(&hist[digit_of(v.z, shift)], 1u);
+            atomicAdd(&hist[digit_of(v.w, shift)], 1u);
+        } else {
+            for (long long j = i; j < b1; ++j) atomicAdd(&hist[digit_of(keys[j], shift)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < kBins; d += kSortThreads) counts[(size_t)d * nblocks + blockIdx.x] = hist[d];
+}
+
+// Stable rank of each lane's digit among the lanes of its wave (ballot match).
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRadixBits; ++b) {
+        const uint64_t m = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? m : ~m;
+    }
+    return peers;
+}
+
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
+    const uint32_t* __restrict__ keys_in, uint32_t* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ vals_out, long long n, long long chunk, int shift, int nblocks,
+    const uint32_t* __restrict__ offsets) {
+    __shared__ uint32_t s_keys[kSortTile];
+    __shared__ uint32_t s_vals[HAS_VALUES ? kSortTile : 1];
+    __shared__ uint32_t s_whist[kSortWaves][kBins];  // per-wave running counts, then exclusive prefixes
+    __shared__ uint32_t s_tile_off[kBins];            // exclusive prefix of tile digit counts
+    __shared__ uint32_t s_base[kBins];                // global position of the next key of each digit
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const long long b0 = (long long)blockIdx.x * chunk;
+    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    for (int d = threadIdx.x; d < kBins; d += kSortThreads) s_base[d] = offsets[(size_t)d * nblocks + blockIdx.x];
+
+    for (long long t0 = b0; t0 < b1; t0 += kSortTile) {
+        for (int d = threadIdx.x; d < kBins; d += kSortThreads)
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) s_whist[w][d] = 0;
+        __syncthreads();
+        // warp-striped: item k of lane l = key t0 + wid*1024 + k*64 + l (memory order = (k, l))
+        uint32_t key[kItems], val[kItems], rank[kItems];
+        // issue all 16 loads first (the ranking below is LDS-serial)
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
+            const bool ok = i < b1;
+            key[k] = ok ? keys_in[i] : 0xffffffffu;
+            if constexpr (HAS_VALUES) val[k] = ok ? vals_in[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
+            const bool ok = i < b1;
+            const uint32_t d = digit_of(key[k], shift);
+            const uint64_t peers = match_digit(d, ok);
+            const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
+            const uint32_t prev = ok ? s_whist[wid][d] : 0u;
+            rank[k] = prev + below;
+            // the lowest lane of each peer group publishes the new running count
+            if (ok && below == 0) s_whist[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
+            if (!ok) rank[k] = 0xffffffffu;
+        }
+        __syncthreads();
+        // per digit: exclusive prefix across waves, tile totals, tile offsets
+        for (int d = threadIdx.x; d < kBins; d += kSortThreads) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) {
+                const uint32_t c = s_whist[w][d];
+                s_whist[w][d] = run;
+                run += c;
+            }
+            s_tile_off[d] = run;  // tile count (made exclusive below)
+        }
+        __syncthreads();
+        // exclusive scan of the 256 tile counts (one value per thread)
+        {
+            __shared__ uint32_t s_tmp[kSortWaves];
+            uint32_t tot;
+            const uint32_t c = s_tile_off[threadIdx.x];
+            const uint32_t ex = block_exclusive_scan<kSortWaves>(c, s_tmp, tot, OpAdd());
+            __syncthreads();
+            s_tile_off[threadIdx.x] = ex;
+        }
+        __syncthreads();
+        // reorder the tile by digit in LDS
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            if (rank[k] != 0xffffffffu) {
+                const uint32_t d = digit_of(key[k], shift);
+                const uint32_t pos = s_tile_off[d] + s_whist[wid][d] + rank[k];
+                s_keys[pos] = key[k];
+                if constexpr (HAS_VALUES) s_vals[pos] = val[k];
+            }
+        }
+        __syncthreads();
+        const int tile_n = (int)((b1 - t0) < kSortTile ? (b1 - t0) : kSortTile);
+        for (int i = threadIdx.x; i < tile_n; i += kSortThreads) {
+            const uint32_t k = s_keys[i];
+            const uint32_t d = digit_of(k, shift);
+            const uint32_t g = s_base[d] + (uint32_t)i - s_tile_off[d];
+            keys_out[g] = k;
+            if constexpr (HAS_VALUES) vals_out[g] = s_vals[i];
+        }
+        __syncthreads();
+        // advance the per-digit bases by this tile's counts
+        {
+            const int d = threadIdx.x;
+            const uint32_t next = d + 1 < kBins ? s_tile_off[d + 1] : (uint32_t)tile_n;
+            s_base[d] += next - s_tile_off[d];
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------ merge sort
+// Block-local bitonic sort of 1024-key tiles (4 keys per thread) in LDS.
+constexpr int kMsTile = 1024;
+
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(256) void bitonic_tile_kernel(uint32_t* keys, uint32_t* vals, long long n) {
+    __shared__ uint32_t sk[kMsTile];
+    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
+    const long long base = (long long)blockIdx.x * kMsTile;
+    for (int i = threadIdx.x; i < kMsTile; i += 256) {
+        const bool ok = base + i < n;
+        sk[i] = ok ? keys[base + i] : 0xffffffffu;
+        if constexpr (HAS_VALUES) sv[i] = ok ? vals[base + i] : 0u;
+    }
+    __syncthreads();
+    for (int size = 2; size <= kMsTile; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < kMsTile / 2; t += 256) {
+                const int i = 2 * t - (t & (stride - 1));
+                const int j = i + stride;
+                const bool up = ((i & size) == 0);
+                const uint32_t a = sk[i], b = sk[j];
+                // stable tie-break is impossible in bitonic; ties keep order
+                // within a key only for keys (values of equal keys may swap)
+                if ((a > b) == up) {
+                    sk[i] = b;
+                    sk[j] = a;
+                    if constexpr (HAS_VALUES) {
+                        const uint32_t x = sv[i];
+                        sv[i] = sv[j];
+                        sv[j] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < kMsTile; i += 256)
+        if (base + i < n) {
+            keys[base + i] = sk[i];
+            if constexpr (HAS_VALUES) vals[base + i] = sv[i];
+        }
+}
+
+// Merge path: merge pairs of sorted runs of length `run` from src into dst.
+// Each lane produces kMP consecutive outputs: it finds its diagonal split by
+// binary search (upper/lower bound, A-first on ties: stable) then merges.
+constexpr int kMP = 8;
+
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(256) void merge_pass_kernel(const uint32_t* __restrict__ sk, uint32_t* __restrict__ dk,
+                                                         const uint32_t* __restrict__ sv, uint32_t* __restrict__ dv,
+                                                         long long n, long long run) {
+    const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const long long out0 = tid * kMP;
+    if (out0 >= n) return;
+    const long long pair = out0 / (2 * run);
+    const long long a0 = pair * 2 * run;
+    const long long a1 = a0 + run < n ? a0 + run : n;
+    const long long b1 = a1 + run < n ? a1 + run : n;
+    const long long la = a1 - a0, lb = b1 - a1;
+    const long long diag = out0 - a0;
+    // find i in [max(0, diag-lb), min(diag, la)] with A[i-1] <= B[diag-i] and B[diag-i-1] < A[i]
+    long long lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if (sk[a0 + mid] <= sk[a1 + diag - mid - 1]) lo = mid + 1;
+        else hi = mid;
+    }
+    long long i = lo, j = diag - lo;
+    const long long end = out0 + kMP < b1 ? out0 + kMP : b1;
+    for (long long o = out0; o < end; ++o) {
+        const bool take_a = (i < la) && (j >= lb || sk[a0 + i] <= sk[a1 + j]);
+        if (take_a) {
+            dk[o] = sk[a0 + i];
+            if constexpr (HAS_VALUES) dv[o] = sv[a0 + i];
+            ++i;
+        } else {
+            dk[o] = sk[a1 + j];
+            if constexpr (HAS_VALUES) dv[o] = sv[a1 + j];
+            ++j;
+        }
+    }
+}
+
+}  // namespace
+
+CME_EXPORT long long cme_radix_ws_bytes(long long n) {
+    long long tiles = (n + kSortTile - 1) / kSortTile;
+    long long nb = tiles < 1024 ? tiles : 1024;
+    return nb * kBins * 4 * 2 + 65536;
+}
+
+// from scan.hip (reduce-then-scan, deterministic)
+extern "C" int cme_scan_rts(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream);
+
+// LSD radix sort of uint32 keys (and optional uint32 values) over bits
+// [bit0, bit1). Ping-pongs between (keys, keys_alt); the sorted output is
+// left in `keys` (copied back after an odd number of passes).
+// ws: cme_radix_ws_bytes(n) bytes.
+CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, long long n,
+                                  int bit0, int bit1, void* ws, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 1) return 0;
+    const long long tiles = (n + kSortTile - 1) / kSortTile;
+    int nb = tiles < 1024 ? (int)tiles : 1024;
+    const long long chunk = ((tiles + nb - 1) / nb) * kSortTile;
+    nb = (int)((n + chunk - 1) / chunk);
+    uint32_t* counts = (uint32_t*)ws;
+    uint32_t* offs = counts + (size_t)nb * kBins;
+    void* scan_ws = offs + (size_t)nb * kBins;
+    uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
+    int passes = 0;
+    for (int shift = bit0; shift < bit1; shift += kRadixBits, ++passes) {
+        hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts);
+        int rc = cme_scan_rts(counts, offs, (long long)nb * kBins, 2, 1, scan_ws, stream);
+        if (rc) return rc;
+        if (vals)
+            hipLaunchKernelGGL(radix_downsweep_kernel<true>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
+                               chunk, shift, nb, offs);
+        else
+            hipLaunchKernelGGL(radix_downsweep_kernel<false>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
+                               chunk, shift, nb, offs);
+        CME_TRY(hipGetLastError());
+        uint32_t* t = ki;
+        ki = ko;
+        ko = t;
+        t = vi;
+        vi = vo;
+        vo = t;
+    }
+    if (passes & 1) {
+        CME_TRY(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToDevice, s));
+        if (vals) CME_TRY(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToDevice, s));
+    }
+    CME_LAUNCH_STATUS();
+}
+
+// Merge sort: bitonic 1024-key tiles, then merge-path passes. Result in keys.
+CME_EXPORT int cme_merge_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, long long n,
+                                  void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 1) return 0;
+    const unsigned tiles = cdiv(n, kMsTile);
+    if (vals) hipLaunchKernelGGL(bitonic_tile_kernel<true>, dim3(tiles), dim3(256), 0, s, keys, vals, n);
+    else hipLaunchKernelGGL(bitonic_tile_kernel<false>, dim3(tiles), dim3(256), 0, s, keys, vals, n);
+    CME_TRY(hipGetLastError());
+    uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
+    int passes = 0;
+    for (long long run = kMsTile; run < n; run <<= 1, ++passes) {
+        const unsigned grid = cdiv(cdiv(n, kMP), 256);
+        if (vals) hipLaunchKernelGGL(merge_pass_kernel<true>, dim3(grid), dim3(256), 0, s, ki, ko, vi, vo, n, run);
+        else hipLaunchKernelGGL(merge_pass_kernel<false>, dim3(grid), dim3(256), 0, s, ki, ko, vi, vo, n, run);
+        CME_TRY(hipGetLastError());
+        uint32_t* t = ki;
+        ki = ko;
+        ko = t;
+        t = vi;
+        vi = vo;
+        vo = t;
+    }
+    if (passes & 1) {
+        CME_TRY(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToDevice, s));
+        if (vals) CME_TRY(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToDevice, s));
+    }
+    CME_LAUNCH_STATUS();
+}

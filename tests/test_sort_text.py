@@ -1,0 +1,98 @@
+"""Sorts (GPU radix/merge, OpenMP radix/merge) and the hw3 text pipeline."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cme213x.models.vigenere import create_cipher, solve_cipher
+from cme213x.ops.sort import merge_sort_cpu, sort
+from cme213x.ops.text import (digraph_histogram, histogram_u8, letter_histogram, match_counts,
+                              residue_histograms, sanitize, vigenere)
+
+BOOK = "/root/reference/hw/hw3/programming/mobydick.txt"
+
+
+def _book():
+    if os.path.exists(BOOK):
+        return open(BOOK, "rb").read()
+    rng = np.random.default_rng(0)
+    words = ["the", "whale", "sea", "ship", "captain", "ahab", "white", "and", "of", "to"]
+    return " ".join(rng.choice(words, 200000)).encode()
+
+
+@pytest.mark.parametrize("algo", ["radix", "radix_serial"])
+@pytest.mark.parametrize("bits", [4, 8, 11, 16])
+def test_cpu_radix(algo, bits):
+    x = torch.randint(0, 2**31 - 1, (50001,), dtype=torch.int32)
+    assert torch.equal(sort(x, algo=algo, num_bits=bits), torch.sort(x).values)
+
+
+@pytest.mark.parametrize("thr", [(1, 2), (100, 100), (10000, 64)])
+def test_cpu_merge(thr):
+    x = torch.randint(-1000, 1000, (100003,), dtype=torch.int32)
+    y, st = merge_sort_cpu(x, *thr)
+    assert st in (1, -1) and torch.equal(y, torch.sort(x).values)
+
+
+def test_text_pipeline_cpu():
+    book = _book()
+    clean = sanitize(torch.from_numpy(np.frombuffer(book, np.uint8).copy()))
+    if os.path.exists(BOOK):
+        assert clean.numel() == 967673  # hw3 writeup: sanitized moby dick length
+        h = letter_histogram(clean).numpy() / clean.numel()
+        assert abs(h[4] - 0.12294) < 1e-4  # 'e' frequency from the writeup
+    c, key = create_cipher(book, 53, device="cpu", out_path=None)
+    r = solve_cipher(c, device="cpu", out_path=None, verbose=False)
+    assert r["key_length"] == 53 and np.array_equal(r["shifts"], key % 26)
+    assert np.array_equal(r["plain"], clean.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 4096, 100003, 3_000_001])
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+def test_gpu_sort_keys(gpu, n, dtype, algo):
+    x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32) if dtype == torch.int32 else torch.randn(n)
+    y = sort(x.to(gpu), algo=algo).cpu()
+    assert torch.equal(y, torch.sort(x).values)
+
+
+@pytest.mark.gpu
+def test_gpu_radix_key_value_stable(gpu):
+    n = 1_000_003
+    k = torch.randint(0, 1000, (n,), dtype=torch.int32)  # many duplicates
+    v = torch.arange(n, dtype=torch.int32)
+    ks, vs = sort(k.to(gpu), v.to(gpu), algo="radix")
+    ref = torch.sort(k, stable=True)
+    assert torch.equal(ks.cpu(), ref.values) and torch.equal(vs.cpu(), ref.indices.to(torch.int32))
+
+
+@pytest.mark.gpu
+def test_gpu_text_kernels(gpu):
+    book = _book()
+    raw = torch.from_numpy(np.frombuffer(book, np.uint8).copy())
+    clean_c = sanitize(raw)
+    clean_g = sanitize(raw.to(gpu))
+    assert torch.equal(clean_g.cpu(), clean_c)
+    assert torch.equal(histogram_u8(raw.to(gpu)).cpu(), histogram_u8(raw))
+    assert torch.equal(letter_histogram(clean_g).cpu(), letter_histogram(clean_c))
+    assert torch.equal(digraph_histogram(clean_g).cpu(), digraph_histogram(clean_c))
+    for p in (7, 500, 3000):
+        assert torch.equal(residue_histograms(clean_g, p).cpu(), residue_histograms(clean_c, p))
+    small = clean_c[:200000]
+    assert torch.equal(match_counts(small.to(gpu), 1, 50).cpu(), match_counts(small, 1, 50))
+    assert torch.equal(match_counts(small.to(gpu), 1990, 40).cpu(), match_counts(small, 1990, 40))
+    key = torch.randint(1, 26, (123,), dtype=torch.int32)
+    enc = vigenere(clean_g, key)
+    assert torch.equal(enc.cpu(), vigenere(clean_c, key))
+    assert torch.equal(vigenere(enc, key, decode=True).cpu(), clean_c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("period", [11, 500])
+def test_gpu_vigenere_roundtrip(gpu, period):
+    book = _book()
+    c, key = create_cipher(book, period, device=gpu, out_path=None)
+    r = solve_cipher(c, device=gpu, out_path=None, verbose=False)
+    assert r["key_length"] == period and np.array_equal(r["shifts"], key % 26)
