@@ -110,6 +110,12 @@ def main():
     if want("spmv"):
         bench_spmv(emit, timeit)
 
+    if want("sort"):
+        bench_sort(emit, timeit)
+
+    if want("vigenere"):
+        bench_vigenere(emit, timeit)
+
     if want("pagerank"):
         from cme213x.ops.graph import bytes_model, iterate, make_graph
 
@@ -161,6 +167,53 @@ def bench_spmv(emit, timeit):
             ref = 39.6 if (name.startswith("27pt") and f == "dia") else (24.2 if f == "hyb" and name == "random-1M" else None)
             emit(bench="spmv", matrix=name, fmt=f, nnz=a.nnz, ms=ms, GFLOPs=2 * a.nnz / ms / 1e6, ref_GFLOPs=ref,
                  vs_ref=(2 * a.nnz / ms / 1e6 / ref) if ref else None)
+
+
+def bench_sort(emit, timeit):
+    import torch
+
+    from cme213x.ops.sort import sort
+
+    for n, ref_s, ref_name in ((16_000_000, 0.084, "radix 16M keys, 32 OpenMP threads (BASELINE #16)"),
+                               (48_000_000, 0.617, "merge sort 48M ints, 32 threads (BASELINE #15)")):
+        x = torch.randint(0, 2**31 - 1, (n,), dtype=torch.int32, device="cuda")
+        for algo in ("radix", "merge"):
+            ms = timeit(lambda: sort(x, algo=algo), iters=5)
+            emit(bench="sort", algo=algo, n=n, ms=ms, Mkeys_per_s=n / ms / 1e3, ref_ms=ref_s * 1e3, ref=ref_name,
+                 speedup_vs_ref=ref_s * 1e3 / ms)
+        ms = timeit(lambda: torch.sort(x), iters=5)
+        emit(bench="sort", algo="torch.sort", n=n, ms=ms, Mkeys_per_s=n / ms / 1e3)
+
+
+def bench_vigenere(emit, timeit):
+    import os
+
+    import numpy as np
+
+    from cme213x.models.vigenere import create_cipher, solve_cipher
+
+    path = "/root/reference/hw/hw3/programming/mobydick.txt"
+    if os.path.exists(path):
+        book = open(path, "rb").read()
+    else:  # English-frequency synthetic corpus of the same size
+        rng = np.random.default_rng(0)
+        en = np.array([8.17, 1.49, 2.78, 4.25, 12.70, 2.23, 2.02, 6.09, 6.97, 0.15, 0.77, 4.03, 2.41, 6.75, 7.51,
+                       1.93, 0.10, 5.99, 6.33, 9.06, 2.76, 0.98, 2.36, 0.15, 1.97, 0.07])
+        book = rng.choice(np.arange(97, 123, dtype=np.uint8), 1_235_150, p=en / en.sum()).tobytes()
+    c, key = create_cipher(book, 500, device="cuda", out_path=None)
+    import time
+
+    import torch
+
+    solve_cipher(c, device="cuda", out_path=None, verbose=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        r = solve_cipher(c, device="cuda", out_path=None, verbose=False)
+    torch.cuda.synchronize()
+    secs = time.perf_counter() - t0
+    emit(bench="vigenere_solve_x10", key_length=r["key_length"], seconds=secs, ref_seconds=17.0,
+         speedup_vs_ref=17.0 / secs)
 
 
 if __name__ == "__main__":
