@@ -1,0 +1,176 @@
+// SGEMM ladder (slides/Lecture09 slides 5-18): C = alpha*A*B + beta*C,
+// row-major A[M][K], B[K][N], C[M][N], fp32.
+//
+//  naive : one lane per C element, K-loop from global memory (matrixMul_slow)
+//  lds   : 64x64 block tile, BK=16, LDS staging, 4x4 register blocking per
+//          lane (the lecture's shared-memory tiled kernel, on the f32 VALU)
+//  mfma  : 128x128x32 block tile on the matrix cores with the exact-f32
+//          v_mfma_f32_32x32x2_f32 (same 64 FLOP/clk/SIMD as the VALU peak but
+//          no VALU issue pressure), 4 waves as 2x2, each 64x64 = 2x2 MFMA
+//          tiles; register-prefetched double-buffered LDS; XCD-aware block
+//          remap. Requires M, N % 128 == 0 and K % 32 == 0 (else `lds`).
+#include "cme213/common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void sgemm_naive_kernel(int M, int N, int K, float alpha, const float* __restrict__ A,
+                                                          const float* __restrict__ B, float beta,
+                                                          float* __restrict__ C) {
+    const int col = blockIdx.x * 64 + threadIdx.x % 64;
+    const int row = blockIdx.y * 4 + threadIdx.x / 64;
+    if (row >= M || col >= N) return;
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += A[(size_t)row * K + k] * B[(size_t)k * N + col];
+    C[(size_t)row * N + col] = alpha * s + (beta == 0.f ? 0.f : beta * C[(size_t)row * N + col]);
+}
+
+constexpr int LT = 64, LK = 16;
+__global__ __launch_bounds__(256) void sgemm_lds_kernel(int M, int N, int K, float alpha, const float* __restrict__ A,
+                                                        const float* __restrict__ B, float beta,
+                                                        float* __restrict__ C) {
+    __shared__ float As[LK][LT + 1];  // k-major, padded
+    __shared__ float Bs[LK][LT];
+    const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;  // 16 x 16 lanes, 4x4 outputs each
+    const int r0 = blockIdx.y * LT, c0 = blockIdx.x * LT;
+    float acc[4][4] = {};
+    for (int k0 = 0; k0 < K; k0 += LK) {
+        for (int i = threadIdx.x; i < LT * LK; i += 256) {
+            const int r = i / LK, k = i % LK;  // A tile: row r, col k
+            As[k][r] = (r0 + r < M && k0 + k < K) ? A[(size_t)(r0 + r) * K + k0 + k] : 0.f;
+            const int kb = i / LT, c = i % LT;  // B tile: row kb, col c
+            Bs[kb][c] = (k0 + kb < K && c0 + c < N) ? B[(size_t)(k0 + kb) * N + c0 + c] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < LK; ++k) {
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[k][ty * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[k][tx * 4 + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = r0 + ty * 4 + i, c = c0 + tx * 4 + j;
+            if (r < M && c < N)
+                C[(size_t)r * N + c] = alpha * acc[i][j] + (beta == 0.f ? 0.f : beta * C[(size_t)r * N + c]);
+        }
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int MT = 128, MK = 32, APAD = MT + 1;
+
+__global__ __launch_bounds__(256) void sgemm_mfma_kernel(int M, int N, int K, float alpha, const float* __restrict__ A,
+                                                         const float* __restrict__ B, float beta,
+                                                         float* __restrict__ C) {
+    __shared__ float As[2][MK * APAD];  // [k][row], padded
+    __shared__ float Bs[2][MK * MT];    // [k][col]
+    const int t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const unsigned nbx = N / MT, nby = M / MT;
+    const unsigned lin = xcd_remap(blockIdx.x, nbx * nby);
+    const int bx = lin % nbx, by = lin / nbx;
+    const int r0 = by * MT, c0 = bx * MT;
+
+    float4 ra[4], rb[4];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = t / 8 + 32 * i, k4 = (t % 8) * 4;
+            ra[i] = *reinterpret_cast<const float4*>(A + (size_t)(r0 + r) * K + k0 + k4);
+            const int kb = t / 32 + 8 * i, n4 = (t % 32) * 4;
+            rb[i] = *reinterpret_cast<const float4*>(B + (size_t)(k0 + kb) * N + c0 + n4);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = t / 8 + 32 * i, k4 = (t % 8) * 4;
+            As[buf][(k4 + 0) * APAD + r] = ra[i].x;
+            As[buf][(k4 + 1) * APAD + r] = ra[i].y;
+            As[buf][(k4 + 2) * APAD + r] = ra[i].z;
+            As[buf][(k4 + 3) * APAD + r] = ra[i].w;
+            const int kb = t / 32 + 8 * i, n4 = (t % 32) * 4;
+            *reinterpret_cast<float4*>(&Bs[buf][kb * MT + n4]) = rb[i];
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    const int lrow = lane & 31, lk = lane >> 5;
+    for (int k0 = 0; k0 < K; k0 += MK) {
+        const bool more = k0 + MK < K;
+        if (more) gload(k0 + MK);  // prefetch next tile into registers
+#pragma unroll
+        for (int kk = 0; kk < MK; kk += 2) {
+            float a[2], b[2];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) a[m] = As[buf][(kk + lk) * APAD + wm * 64 + m * 32 + lrow];
+#pragma unroll
+            for (int n = 0; n < 2; ++n) b[n] = Bs[buf][(kk + lk) * MT + wn * 64 + n * 32 + lrow];
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int n = 0; n < 2; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m], b[n], acc[m][n], 0, 0, 0);
+        }
+        if (more) {
+            lstore(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+    }
+    // C/D map: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = r0 + wm * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int col = c0 + wn * 64 + n * 32 + (lane & 31);
+                float* cp = C + (size_t)row * N + col;
+                *cp = alpha * acc[m][n][r] + (beta == 0.f ? 0.f : beta * *cp);
+            }
+}
+
+}  // namespace
+
+// variant: 0 naive, 1 lds, 2 mfma (falls back to lds when shapes don't tile)
+CME_EXPORT int cme_sgemm(int M, int N, int K, float alpha, const float* A, const float* B, float beta, float* C,
+                         int variant, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (variant == 2 && (M % MT || N % MT || K % MK || ((uintptr_t)A % 16) || ((uintptr_t)B % 16))) variant = 1;
+    switch (variant) {
+        case 0:
+            hipLaunchKernelGGL(sgemm_naive_kernel, dim3(cdiv(N, 64), cdiv(M, 4)), dim3(256), 0, s, M, N, K, alpha, A,
+                               B, beta, C);
+            break;
+        case 1:
+            hipLaunchKernelGGL(sgemm_lds_kernel, dim3(cdiv(N, LT), cdiv(M, LT)), dim3(256), 0, s, M, N, K, alpha, A, B,
+                               beta, C);
+            break;
+        case 2:
+            hipLaunchKernelGGL(sgemm_mfma_kernel, dim3((M / MT) * (N / MT)), dim3(256), 0, s, M, N, K, alpha, A, B,
+                               beta, C);
+            break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
