@@ -116,6 +116,12 @@ def main():
     if want("vigenere"):
         bench_vigenere(emit, timeit)
 
+    if want("gemm"):
+        bench_gemm(emit, timeit)
+
+    if want("misc"):
+        bench_misc(emit, timeit)
+
     if want("pagerank"):
         from cme213x.ops.graph import bytes_model, iterate, make_graph
 
@@ -214,6 +220,46 @@ def bench_vigenere(emit, timeit):
     secs = time.perf_counter() - t0
     emit(bench="vigenere_solve_x10", key_length=r["key_length"], seconds=secs, ref_seconds=17.0,
          speedup_vs_ref=17.0 / secs)
+
+
+def bench_gemm(emit, timeit):
+    import torch
+
+    from cme213x.ops.gemm import sgemm
+
+    ref = {"naive": 80.0, "lds": 235.9, "mfma": 784.6}  # GTX 480 GFLOP/s (Lecture09; mfma vs CUBLAS)
+    for n in (1024, 4096, 8192):
+        A = torch.randn(n, n, device="cuda")
+        B = torch.randn_like(A)
+        C = torch.empty_like(A)
+        for v in (("naive",) if n <= 4096 else ()) + ("lds", "mfma"):
+            ms = timeit(lambda: sgemm(A, B, C, variant=v), iters=3, warmup=1)
+            gf = 2 * n ** 3 / ms / 1e6
+            emit(bench="sgemm", n=n, variant=v, ms=ms, GFLOPs=gf, ref_GFLOPs=ref[v], vs_ref=gf / ref[v])
+        torch.backends.cuda.matmul.allow_tf32 = False
+        ms = timeit(lambda: torch.mm(A, B, out=C), iters=3, warmup=1)
+        emit(bench="sgemm", n=n, variant="torch.mm(hipBLASLt)", ms=ms, GFLOPs=2 * n ** 3 / ms / 1e6)
+
+
+def bench_misc(emit, timeit):
+    import math
+
+    import torch
+
+    from cme213x.ops.atomics import global_max, monte_carlo_pi
+
+    n = 1 << 30
+    import time
+
+    monte_carlo_pi(1 << 20, 1, "cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pi, _ = monte_carlo_pi(n, 3, "cuda")
+    dt = time.perf_counter() - t0
+    emit(bench="monte_carlo_pi", samples=n, seconds=dt, Gsamples_per_s=n / dt / 1e9, err=abs(pi - math.pi))
+    x = torch.randn(1 << 26, device="cuda")
+    ms = timeit(lambda: global_max(x))
+    emit(bench="global_max", n=x.numel(), ms=ms, GBps=4 * x.numel() / ms / 1e6)
 
 
 if __name__ == "__main__":

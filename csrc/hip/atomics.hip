@@ -59,10 +59,11 @@ __global__ __launch_bounds__(256) void workqueue_kernel(const int* __restrict__ 
                                                         const float* __restrict__ v, float* __restrict__ out,
                                                         unsigned* __restrict__ head) {
     const int lane = lane_id();
-    while (true) {
-        int seg = 0;
-        if (lane == 0) seg = (int)atomicAdd(head, 1u);  // dequeue one segment per wave
-        seg = __builtin_amdgcn_readfirstlane(seg);
+    // bounded: a wave can never dequeue more than nseg + 1 times
+    for (int iter = 0; iter <= nseg; ++iter) {
+        unsigned t = 0;
+        if (lane == 0) t = atomicAdd(head, 1u);  // dequeue one segment per wave
+        const int seg = (int)__shfl(t, 0, kWave);
         if (seg >= nseg) return;  // every wave reaches this exit
         const int b = offsets[seg], e = offsets[seg + 1];
         float s = 0.f;
