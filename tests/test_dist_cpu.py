@@ -77,3 +77,74 @@ def test_collectives_gloo():
         assert bc == 10
         assert ssz == 2 and ss == 2.0
         assert a2a == [float(r + 100 * k) for k in range(4)]
+
+
+def _dist_spmv_rank(rank, world, mode):
+    import cme213x
+    from cme213x.models.dist_spmv import RowPartitionedSpMV
+    from cme213x.ops.spmv import random_csr, spmv
+    from cme213x.parallel.comm import TorchComm
+
+    a = random_csr(3000, 3000, 9, seed=4)
+    x = torch.from_numpy(np.random.default_rng(0).standard_normal(3000).astype(np.float32))
+    op = RowPartitionedSpMV(a, TorchComm(), "cpu", mode=mode)
+    y = op(op.local_slice(x))
+    ref = spmv(a, x)
+    return (op.lo, op.hi, y.numpy(), ref.numpy()[op.lo:op.hi])
+
+
+@pytest.mark.parametrize("mode", ["allgather", "halo"])
+def test_row_partitioned_spmv_gloo(mode):
+    for lo, hi, y, ref in run_ranks(_dist_spmv_rank, 4, (mode,)):
+        np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
+
+
+def _dense_matvec_rank(rank, world):
+    import cme213x
+    from cme213x.models.dist_spmv import block2d_matvec, colwise_matvec
+    from cme213x.parallel.comm import TorchComm
+
+    c = TorchComm()
+    n = 64
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(n, n, generator=g, dtype=torch.float64)
+    x = torch.randn(n, generator=g, dtype=torch.float64)
+    nb = n // world
+    ycol = colwise_matvec(c, A[:, rank * nb:(rank + 1) * nb].contiguous(), x[rank * nb:(rank + 1) * nb].contiguous())
+    q = 2
+    row, col = divmod(rank, q)
+    bs = n // q
+    Ab = A[row * bs:(row + 1) * bs, col * bs:(col + 1) * bs].contiguous()
+    xd = x[row * bs:(row + 1) * bs].clone() if row == col else None
+    y2 = block2d_matvec(c, Ab, xd)
+    ref = A @ x
+    ok_col = torch.allclose(ycol, ref[rank * nb:(rank + 1) * nb])
+    ok_2d = (y2 is None) or torch.allclose(y2, ref[row * bs:(row + 1) * bs])
+    return ok_col, ok_2d
+
+
+def test_dense_matvecs_gloo():
+    for ok_col, ok_2d in run_ranks(_dense_matvec_rank, 4):
+        assert ok_col and ok_2d
+
+
+def _p2p_collectives_rank(rank, world):
+    import cme213x
+    from cme213x.parallel.collectives import ring_allgather, tree_broadcast, tree_reduce_sum
+    from cme213x.parallel.comm import TorchComm
+
+    c = TorchComm()
+    g = ring_allgather(c, torch.tensor([rank * 1.0, rank + 0.5]))
+    b = tree_broadcast(c, torch.tensor([float(rank)] * 3), root=2)
+    r = tree_reduce_sum(c, torch.tensor([float(rank + 1)]), root=1)
+    return g.tolist(), b.tolist(), r.item()
+
+
+def test_p2p_collectives_gloo():
+    world = 5
+    out = run_ranks(_p2p_collectives_rank, world)
+    for rank, (g, b, r) in enumerate(out):
+        assert g == [[k * 1.0, k + 0.5] for k in range(world)]
+        assert b == [2.0] * 3
+        if rank == 1:
+            assert r == sum(range(1, world + 1))
