@@ -115,7 +115,10 @@ def _link(objs: list[Path], out: Path, kind: str) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_suffix(".so.tmp")
     if kind == "hip":
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        # librccl.so.1 resolves to the RCCL instance torch has already loaded
+        rocm_lib = os.environ.get("ROCM_PATH", "/opt/rocm") + "/lib"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
+               f"-L{rocm_lib}", "-lrccl"]
     else:
         cmd = [CXX, "-shared", "-fPIC", "-fopenmp", "-o", str(tmp), *map(str, objs)]
     _run(cmd)

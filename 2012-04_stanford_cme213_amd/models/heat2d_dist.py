@@ -181,6 +181,67 @@ class DistHeat:
             s.grid.iteration += 1
         self.iteration += 1
 
+    # -- native loop (RCCL + HIP, no per-step Python) ---------------------
+    def _native_plan(self):
+        if getattr(self, "_plan", None) is not None:
+            return self._plan
+        import numpy as np
+
+        (r, s), = self.subs.items()
+        g, b = s.grid, s.blk
+        B, ny, pitch = g.B, g.ny, g.pitch
+        interior = [reg for reg in _interior_regions(s)]
+        border = [reg for reg in _border_regions(s)]
+        rows, cols = [], []
+        for side in ("top", "bottom"):
+            peer = getattr(b, side)
+            if peer >= 0:
+                send = (ny if side == "top" else B) * pitch
+                recv = (ny + B if side == "top" else 0) * pitch
+                rows.append((peer, send, recv, B * pitch))
+        for side in ("left", "right"):
+            peer = getattr(b, side)
+            if peer >= 0:
+                sx = g.nx if side == "right" else B
+                rx = g.nx + B if side == "right" else 0
+                cols.append((peer, sx, rx, B, ny, B))
+        stage_elems = 2 * sum(c[4] * c[5] for c in cols)
+        plan = {
+            "interior": torch.tensor(np.array(interior, dtype=np.int32).reshape(-1, 4)),
+            "border": torch.tensor(np.array(border, dtype=np.int32).reshape(-1, 4)),
+            "rows": torch.tensor(np.array(rows, dtype=np.int64).reshape(-1, 4)),
+            "cols": torch.tensor(np.array(cols, dtype=np.int32).reshape(-1, 6)),
+            "stage": torch.empty(max(stage_elems, 1), dtype=g.dtype, device=g.device),
+        }
+        self._plan = plan
+        return plan
+
+    def run_native(self, iters: int, rccl, sync: bool | None = None) -> None:
+        """``iters`` timesteps in ONE native call (RCCL P2P halo exchange on a
+        communication stream, interior/exchange overlap in async mode).
+        ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl`."""
+        import ctypes
+
+        from .. import _ext
+
+        if len(self.subs) != 1:
+            raise ValueError("native loop: one subdomain per process")
+        self.finish()
+        sync = self.p.sync if sync is None else sync
+        plan = self._native_plan()
+        (r, s), = self.subs.items()
+        g = s.grid
+        cur_out = ctypes.c_int(0)
+        _ext.call_hip("cme_heat_dist_run", rccl.handle, g.buf[0].data_ptr(), g.buf[1].data_ptr(), g.pitch, g.gy,
+                      plan["interior"].data_ptr(), plan["interior"].shape[0], plan["border"].data_ptr(),
+                      plan["border"].shape[0], plan["rows"].data_ptr(), plan["rows"].shape[0],
+                      plan["cols"].data_ptr(), plan["cols"].shape[0], plan["stage"].data_ptr(),
+                      0 if g.dtype == torch.float32 else 1, g.order, g.xcfl, g.ycfl, iters, g.cur, int(sync), 0,
+                      ctypes.addressof(cur_out), _ext.stream_ptr(g.device))
+        g.cur = cur_out.value
+        g.iteration += iters
+        self.iteration += iters
+
     def finish(self) -> None:
         pend = getattr(self, "_pending", None)
         if pend is not None:

@@ -16,6 +16,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipipipiiddiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")

@@ -1,0 +1,70 @@
+"""Native RCCL communicator (``ncclCommInitRank`` from C++), bootstrapped
+over an existing torch.distributed group: rank 0 draws the unique id and
+broadcasts it. Used where per-call Python overhead matters (the distributed
+stencil's K-step loop runs entirely in ``cme_heat_dist_run``)."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_unique_id", "p")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_init", "pipi")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_destroy", "p")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_allreduce", "pppqiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_allgather", "pppqip")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_p2p", "pippppip")
+
+_DT = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4}
+_OP = {"sum": 0, "max": 1, "min": 2, "prod": 3}
+
+
+class NativeRccl:
+    def __init__(self, group=None):
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed must be initialised first")
+        self.rank = dist.get_rank(group)
+        self.size = dist.get_world_size(group)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            _ext.call_hip("cme_rccl_unique_id", ctypes.addressof(buf))
+            uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        uid_d = uid.to(dev)
+        dist.broadcast(uid_d, dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        raw = bytes(uid_d.cpu().numpy().tobytes())
+        self._id = ctypes.create_string_buffer(raw, 128)
+        h = ctypes.c_void_p()
+        _ext.call_hip("cme_rccl_init", ctypes.addressof(h), self.size, ctypes.addressof(self._id), self.rank)
+        self.handle = h.value
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        _ext.call_hip("cme_rccl_allreduce", self.handle, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op],
+                      _ext.stream_ptr(t.device))
+        return t
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        _ext.call_hip("cme_rccl_allgather", self.handle, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype],
+                      _ext.stream_ptr(t.device))
+        return out
+
+    def p2p(self, ops) -> None:
+        """ops: list of (kind, tensor, peer) in one ncclGroupStart/End."""
+        n = len(ops)
+        peers = (ctypes.c_int * n)(*[o[2] for o in ops])
+        sends = (ctypes.c_int * n)(*[1 if o[0] == "send" else 0 for o in ops])
+        ptrs = (ctypes.c_void_p * n)(*[o[1].data_ptr() for o in ops])
+        cnts = (ctypes.c_longlong * n)(*[o[1].numel() for o in ops])
+        _ext.call_hip("cme_rccl_p2p", self.handle, n, ctypes.addressof(peers), ctypes.addressof(sends),
+                      ctypes.addressof(ptrs), ctypes.addressof(cnts), _DT[ops[0][1].dtype],
+                      _ext.stream_ptr(ops[0][1].device))
+
+    def close(self) -> None:
+        if self.handle:
+            _ext.call_hip("cme_rccl_destroy", self.handle)
+            self.handle = None

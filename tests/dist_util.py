@@ -25,7 +25,7 @@ def _worker(rank, world, port, fn, args, q):
                           WORLD_SIZE=str(world), LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
         import torch.distributed as dist
 
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # gloo default; GPU tests add nccl groups
         out = fn(rank, world, *args)
         dist.barrier()
         dist.destroy_process_group()

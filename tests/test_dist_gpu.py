@@ -1,0 +1,97 @@
+"""Distributed heat on the GPU: the native RCCL loop (cme_heat_dist_run) and
+the torch.distributed (RCCL) path, checked against the single-grid result.
+World size 1 always; world size 2 on the same GPU when RCCL allows two ranks
+per device (skipped otherwise)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dist_util import free_port
+
+
+def _setup_single():
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sync", [True, False])
+def test_native_loop_world1(gpu, sync):
+    import torch.distributed as dist
+
+    from cme213x.models.heat2d import HeatGrid
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.parallel.rccl import NativeRccl
+    from cme213x.utils.params import SimParams
+
+    _setup_single()
+    p = SimParams(nx=300, ny=211, order=8, iters=6, sync=sync, flavor="hw5")
+    sim = DistHeat(p, TorchComm(), torch.float32, gpu)
+    rc = NativeRccl()
+    sim.run_native(6, rc)
+    torch.cuda.synchronize()
+    ref = HeatGrid(p, torch.float32, gpu)
+    ref.run(6, "stream")
+    assert np.array_equal(sim.gather_global(), ref.state().astype(np.float64))
+    x = torch.arange(10, dtype=torch.float32, device=gpu)
+    rc.allreduce_(x)
+    assert torch.equal(x.cpu(), torch.arange(10, dtype=torch.float32))
+    rc.close()
+    dist.destroy_process_group()
+
+
+def _two_ranks_same_gpu(rank, world, method, sync, native):
+    import torch
+    import torch.distributed as dist
+
+    import cme213x
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.parallel.rccl import NativeRccl
+    from cme213x.utils.params import SimParams
+
+    torch.cuda.set_device(0)
+    g = dist.new_group(backend="nccl")
+    comm = TorchComm(g)
+    p = SimParams(nx=260, ny=180, order=8, iters=5, sync=sync, grid_method=method, flavor="hw5")
+    sim = DistHeat(p, comm, torch.float32, "cuda:0")
+    if native:
+        rc = NativeRccl(g)
+        sim.run_native(5, rc)
+    else:
+        sim.run(5)
+    torch.cuda.synchronize()
+    s = next(iter(sim.subs.values()))
+    B = s.grid.B
+    return s.blk.x0, s.blk.y0, s.grid.state()[B:B + s.blk.ny, B:B + s.blk.nx]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("native", [True, False])
+def test_two_ranks_one_gpu(gpu, native):
+    from dist_util import run_ranks
+
+    from cme213x.models.heat2d import HeatGrid
+    from cme213x.utils.params import SimParams
+
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    try:
+        parts = run_ranks(_two_ranks_same_gpu, 2, (1, False, native), timeout=180)
+    except RuntimeError as e:
+        if "Duplicate GPU" in str(e) or "invalid usage" in str(e).lower():
+            pytest.skip("RCCL refuses two ranks on one GPU")
+        raise
+    p = SimParams(nx=260, ny=180, order=8, iters=5, flavor="hw5")
+    ref = HeatGrid(p, torch.float32, gpu)
+    ref.run(5, "stream")
+    st = ref.state()
+    B = p.border
+    for x0, y0, part in parts:
+        np.testing.assert_array_equal(part, st[B + y0:B + y0 + part.shape[0], B + x0:B + x0 + part.shape[1]])
