@@ -31,6 +31,39 @@ sys.path.insert(0, REPO)
 BASELINE_GBPS = 239.7  # heat 4000^2 order 8 LDS kernel, 48.07 ms / 10 iters, 72 B/pt
 
 
+def native_selftest(comm, rccl, dev, args) -> bool:
+    """Run a small problem through the native RCCL loop AND the
+    torch.distributed loop (the path the multi-process CPU tests cover) and
+    require bitwise-equal subdomains on every rank before trusting the native
+    loop for the measurement."""
+    import torch
+
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=1024, ny=1024, iters=6, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
+                  grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
+    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant)
+    b = DistHeat(p, comm, torch.float32, dev, variant=args.variant)
+    # non-uniform interior so a stale or misplaced halo changes the answer
+    for sim in (a, b):
+        s = next(iter(sim.subs.values()))
+        g, B = s.grid, s.grid.B
+        yy = torch.arange(s.blk.ny, device=dev, dtype=torch.float32).view(-1, 1) + s.blk.y0
+        xx = torch.arange(s.blk.nx, device=dev, dtype=torch.float32).view(1, -1) + s.blk.x0
+        g.buf[:, B:B + s.blk.ny, B:B + s.blk.nx] = 5.0 + torch.sin(0.05 * xx) * torch.cos(0.03 * yy)
+        sim.exchange(sim._cur()).wait()
+    a.run_native(6, rccl)
+    for _ in range(6):
+        b.step()
+    b.finish()
+    torch.cuda.synchronize(dev)
+    sa, sb = next(iter(a.subs.values())).grid, next(iter(b.subs.values())).grid
+    bad = torch.tensor([0.0 if torch.equal(sa.buf[sa.cur], sb.buf[sb.cur]) else 1.0], device=dev)
+    comm.allreduce_(bad, "max")
+    return bool(bad.item() == 0)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,6 +74,8 @@ def main() -> int:
     ap.add_argument("--method", type=int, default=1, help="1 = 1-D stripes, 2 = 2-D blocks")
     ap.add_argument("--mode", choices=["async", "sync"], default="async")
     ap.add_argument("--variant", default="stream")
+    ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
+                    help="multi-GPU: run the K-step loop in C++ over a native RCCL communicator")
     args = ap.parse_args()
 
     import torch
@@ -64,21 +99,36 @@ def main() -> int:
 
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
+
+    rccl, native_ok = None, False
+    if comm.size > 1 and args.native != "off":
+        from cme213x.parallel.rccl import NativeRccl
+
+        rccl = NativeRccl()
+        native_ok = True
+        if args.native == "auto":
+            native_ok = native_selftest(comm, rccl, dev, args)
+    use_native = rccl is not None and native_ok
+
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant)
+
+    def run(k):
+        if use_native:
+            sim.run_native(k, rccl)
+        else:
+            for _ in range(k):
+                sim.step()
+            sim.finish()
 
     def barrier_sync():
         torch.cuda.synchronize(dev)
         comm.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
-        sim.step()
-    sim.finish()
+    run(args.warmup)
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sim.step()
-    sim.finish()
+    run(args.steps)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     comm.barrier()
@@ -117,11 +167,13 @@ def main() -> int:
                 "seq_len": 1,
                 "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
                 "variant": args.variant,
+                "loop": "native-rccl" if use_native else ("torch.distributed" if comm.size > 1 else "single"),
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
             "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),
             "gpoints_per_s": round(pts * args.steps / secs / 1e9, 2),
             "sanity_ok": bool(bad.item() == 0),
+            "native_selftest": (native_ok if rccl is not None else None),
         }
         print(json.dumps(rec), flush=True)
     if dist.is_initialized():
