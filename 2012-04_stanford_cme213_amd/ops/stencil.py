@@ -8,21 +8,25 @@ the OpenMP oracle (``csrc/cpu/heat2d_cpu.cpp``). Parity target: the reference's
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from .. import _ext
 
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipipipiiddiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f64", "ppiiiiiiddi")
 
-VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3}
+VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4}
+# variants that advance more than one timestep per launch (multi-step drivers only)
+MULTISTEP = {"stream2"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -42,6 +46,8 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
               xcfl: float, ycfl: float, variant: str = "stream", chunk: int = 0) -> None:
     """curr[region] = FTCS(prev); region = (xb, xe, yb, ye) in grid coords."""
     _check(prev, curr)
+    if variant in MULTISTEP:
+        raise ValueError(f"variant {variant!r} advances two steps per launch; use heat_run")
     xb, xe, yb, ye = map(int, region)
     rows, pitch = prev.shape
     f64 = prev.dtype == torch.float64
@@ -56,16 +62,20 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
 
 def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
              ycfl: float, iters: int, variant: str = "stream", chunk: int = 0) -> torch.Tensor:
-    """``iters`` ping-pong sweeps starting from ``a``; returns the buffer holding
-    the final state (``a`` if iters is even, else ``b``)."""
+    """``iters`` timesteps starting from ``a``; returns the buffer holding the
+    final state. Single-step variants ping-pong (final = ``a`` iff iters is
+    even); ``stream2`` advances two steps per HBM pass (temporal blocking), so
+    the final buffer is reported by the native driver."""
     _check(a, b)
     xb, xe, yb, ye = map(int, region)
     rows, pitch = a.shape
     f64 = a.dtype == torch.float64
     if a.is_cuda:
         name = "cme_heat_run_f64" if f64 else "cme_heat_run_f32"
+        final = ctypes.c_int(0)
         _ext.call_hip(name, a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, VARIANTS[variant],
-                      xcfl, ycfl, iters, chunk, _ext.stream_ptr(a.device))
+                      xcfl, ycfl, iters, chunk, ctypes.addressof(final), _ext.stream_ptr(a.device))
+        return b if final.value else a
     else:
         name = "cme_cpu_heat_run_f64" if f64 else "cme_cpu_heat_run_f32"
         _ext.call_cpu(name, a.data_ptr(), b.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl, iters)

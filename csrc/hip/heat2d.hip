@@ -181,6 +181,112 @@ __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restri
     }
 }
 
+
+// ---------------------------------------------------------------- stream2
+// Temporal blocking: TWO timesteps per pass over HBM. The wave keeps an input
+// row window AND a window of step-1 rows in VGPRs; step-1 rows are produced
+// on lanes 1..62 (x-neighbours through DPP), step-2 rows on lanes 2..61
+// (4 x 60 = 240 output columns per strip). Cells outside the region keep
+// their input value in the intermediate state (fixed boundary cells), so the
+// result is bitwise identical to two single steps.
+constexpr int kStrip2Out = 60 * 4;
+
+template <typename T, int ORDER, int RB>
+__global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+                                                           int gy, int xb, int xe, int yb, int ye, int strips,
+                                                           int chunk, int total_waves, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int NW = RB + 2 * B;
+    const int lane = lane_id();
+    const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
+    if (wave >= total_waves) return;
+    const int strip = wave % strips;
+    const int ck = wave / strips;
+    const int y0 = yb + ck * chunk;
+    const int y1 = min(ye, y0 + chunk);
+    const int xs = (xb & ~3) + strip * kStrip2Out;
+    const int xbase = xs - 8 + 4 * lane;
+    const int xl = min(max(xbase, 0), pitch - 4);
+    const bool out_lane = (lane >= 2) && (lane <= 61) && (xbase < xe) && (xbase + 4 > xb);
+    const bool full_vec = (xbase >= xb) && (xbase + 4 <= xe);
+    const T* src = prev + xl;
+    T* dst = curr + xl;
+    auto row_ptr = [&](int r) -> const T* {
+        r = r < 0 ? 0 : (r >= gy ? gy - 1 : r);
+        return src + (size_t)r * pitch;
+    };
+    // one FTCS update of the 4 columns of this lane for a row whose window is
+    // w[k0 .. k0+2B]; cells outside the region keep their value
+    auto update = [&](const V4<T>* w, int k0, int row) -> V4<T> {
+        const V4<T> c = w[k0 + B];
+        const V4<T> L = wave_shr1(c);
+        const V4<T> R = wave_shl1(c);
+        T rowv[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            rowv[j] = L[j];
+            rowv[4 + j] = c[j];
+            rowv[8 + j] = R[j];
+        }
+        V4<T> o;
+        const bool row_in = row >= yb && row < ye;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                xm[k] = rowv[4 + j - (k + 1)];
+                xp[k] = rowv[4 + j + (k + 1)];
+                ym[k] = w[k0 + B - (k + 1)][j];
+                yp[k] = w[k0 + B + (k + 1)][j];
+            }
+            const T u = heat_update<ORDER>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+            const int x = xbase + j;
+            o[j] = (row_in && x >= xb && x < xe) ? u : c[j];
+        }
+        return o;
+    };
+
+    V4<T> in[NW];   // input rows r0-B .. r0+RB-1+B
+    V4<T> s1[NW];   // step-1 rows r0-2B .. r0+RB-1
+    V4<T> nxt[RB];
+    int r0 = y0 - B;  // first step-1 row of the current block
+#pragma unroll
+    for (int i = 0; i < 2 * B; ++i) in[i] = load4(row_ptr(r0 - B + i));
+#pragma unroll
+    for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + B + i));
+    for (; r0 - B < y1; r0 += RB) {
+#pragma unroll
+        for (int i = 0; i < RB; ++i) in[2 * B + i] = nxt[i];
+        if (r0 + RB - B < y1) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) s1[2 * B + i] = update(in, i, r0 + i);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            const int y = r0 - B + i;
+            const V4<T> o = update(s1, i, y);
+            if (out_lane && y >= y0 && y < y1) {
+                T* d = dst + (size_t)y * pitch;
+                if (full_vec) {
+                    store4(d, o);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (xbase + j >= xb && xbase + j < xe) d[j] = o[j];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2 * B; ++i) {
+            in[i] = in[RB + i];
+            s1[i] = s1[RB + i];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- launchers
 namespace {
 
@@ -203,6 +309,24 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         dim3 grid(cdiv(W, 64), cdiv(H, TY));
         hipLaunchKernelGGL((heat_lds_kernel<T, ORDER, TY, 1>), grid, dim3(256), 0, s, prev, curr, pitch, gy, g.xb,
                            g.xe, g.yb, g.ye, xcfl, ycfl);
+    } else if (variant == 4) {
+        // TWO timesteps per launch (temporal blocking)
+        constexpr int RB = sizeof(T) == 4 ? 4 : 2;
+        const int x_lo = g.xb & ~3;
+        const int strips = (int)cdiv(g.xe - x_lo, kStrip2Out);
+        int chunk = chunk_hint;
+        if (chunk <= 0) {
+            const long target_waves = 256L * 12;
+            long rows = ((long)strips * H + target_waves - 1) / target_waves;
+            rows = rows < 4 * RB ? 4 * RB : rows;
+            rows = rows > 512 ? 512 : rows;
+            chunk = (int)rows;
+        }
+        chunk = ((chunk + RB - 1) / RB) * RB;
+        const int chunks = (int)cdiv(H, chunk);
+        const int total_waves = strips * chunks;
+        hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev,
+                           curr, pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -244,7 +368,7 @@ int dispatch_heat(int order, int variant, const T* prev, T* curr, int pitch, int
 
 }  // namespace
 
-// variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad)
+// variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO steps)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -257,31 +381,46 @@ CME_EXPORT int cme_heat_step_f64(const double* prev, double* curr, int pitch, in
                                  as_stream(stream));
 }
 
-// Multi-step driver: `iters` ping-pong sweeps of the full region in one call
-// (buffers a/b, first sweep reads a). Avoids per-iteration host round trips
-// (the reference synchronises after every launch: 2dHeat_solution.cu:549).
-CME_EXPORT int cme_heat_run_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
-                                int variant, float xcfl, float ycfl, int iters, int chunk, void* stream) {
-    for (int i = 0; i < iters; ++i) {
-        const float* p = (i & 1) ? b : a;
-        float* c = (i & 1) ? a : b;
-        int rc = dispatch_heat<float>(order, variant, p, c, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
-                                      as_stream(stream));
-        if (rc) return rc;
+// Multi-step driver: `iters` sweeps of the full region in one call (buffers
+// a/b, first sweep reads a). Avoids per-iteration host round trips (the
+// reference synchronises after every launch: 2dHeat_solution.cu:549).
+// variant 4 advances TWO steps per launch (+ one single step for odd iters).
+// *final_idx = 0 if the result is in a, 1 if in b.
+template <typename T>
+int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int variant, T xcfl, T ycfl, int iters,
+                  int chunk, int* final_idx, hipStream_t s) {
+    int cur = 0;
+    T* bufs[2] = {a, b};
+    int i = 0;
+    if (variant == 4) {
+        for (; i + 1 < iters; i += 2) {
+            int rc = dispatch_heat<T>(order, 4, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
+            if (rc) return rc;
+            cur ^= 1;
+        }
+        variant = 2;
     }
+    for (; i < iters; ++i) {
+        int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
+        if (rc) return rc;
+        cur ^= 1;
+    }
+    *final_idx = cur;
     return 0;
 }
 
+CME_EXPORT int cme_heat_run_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
+                                int variant, float xcfl, float ycfl, int iters, int chunk, int* final_idx,
+                                void* stream) {
+    return heat_run_impl<float>(a, b, pitch, gy, Region{xb, xe, yb, ye}, order, variant, xcfl, ycfl, iters, chunk,
+                                final_idx, as_stream(stream));
+}
+
 CME_EXPORT int cme_heat_run_f64(double* a, double* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
-                                int variant, double xcfl, double ycfl, int iters, int chunk, void* stream) {
-    for (int i = 0; i < iters; ++i) {
-        const double* p = (i & 1) ? b : a;
-        double* c = (i & 1) ? a : b;
-        int rc = dispatch_heat<double>(order, variant, p, c, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
-                                       as_stream(stream));
-        if (rc) return rc;
-    }
-    return 0;
+                                int variant, double xcfl, double ycfl, int iters, int chunk, int* final_idx,
+                                void* stream) {
+    return heat_run_impl<double>(a, b, pitch, gy, Region{xb, xe, yb, ye}, order, variant, xcfl, ycfl, iters, chunk,
+                                 final_idx, as_stream(stream));
 }
 
 // Tuning entry point for the streaming kernel (order 8, fp32): explores rows

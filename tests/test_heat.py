@@ -128,6 +128,45 @@ def test_gpu_stream_subregion(gpu, region):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("iters", [1, 2, 5])
+def test_gpu_stream2_temporal_blocking_bitwise(gpu, order, dtype, iters):
+    # two steps per HBM pass must equal two single steps bit for bit
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, dtype)
+    g = _rand_grid(p, dtype, gpu)
+    c.run(iters, "naive")
+    g.run(iters, "stream2")
+    torch.cuda.synchronize()
+    d = ulp_distance(c.state(), g.state())
+    assert int(d.max()) == 0, f"max ulp {int(d.max())}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("region", [(4, 300, 4, 100), (9, 250, 17, 77), (130, 131, 5, 200), (8, 292, 8, 242)])
+@pytest.mark.parametrize("chunk", [0, 8, 12])
+def test_gpu_stream2_subregion(gpu, region, chunk):
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    ca, cb = c.buf[0].clone(), c.buf[0].clone()
+    ga, gb = g.buf[0].clone(), g.buf[0].clone()
+    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 4)
+    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 4, "stream2", chunk)
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+
+
+def test_stream2_rejected_for_single_step():
+    p = SimParams(nx=40, ny=30, order=2)
+    c = _rand_grid(p, torch.float32)
+    with pytest.raises(ValueError):
+        c.step("stream2")
+
+
+@pytest.mark.gpu
 def test_hw2_driver_gpu(gpu, tmp_path):
     p = SimParams(nx=200, ny=150, iters=10, order=8)
     f = tmp_path / "params.in"
