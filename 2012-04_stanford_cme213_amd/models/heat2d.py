@@ -34,10 +34,14 @@ class HeatGrid:
     ``border`` cells. ``bc_sides`` selects which sides carry the physical
     boundary condition (all four for a single device; the distributed driver
     passes only the sides with no neighbour, as ``hw/hw5/2dHeat_solution.cpp``
-    does)."""
+    does). ``halo`` (default ``border``) is the allocated ghost depth ``H``;
+    the distributed driver uses ``H = 2*border`` so one exchange feeds two
+    timesteps (temporal blocking). Only the inner ``border`` ghost layers are
+    ever read on physical sides; :meth:`state` always returns the
+    reference-layout grid with a ``border``-deep halo."""
 
     def __init__(self, params: SimParams, dtype=torch.float32, device="cpu", nx: int | None = None,
-                 ny: int | None = None, bc_sides=(True, True, True, True)):
+                 ny: int | None = None, bc_sides=(True, True, True, True), halo: int | None = None):
         self.params = params
         self.dtype = dtype
         self.device = torch.device(device)
@@ -45,34 +49,37 @@ class HeatGrid:
         self.B = params.border
         self.nx = params.nx if nx is None else nx
         self.ny = params.ny if ny is None else ny
-        if self.nx <= 2 * self.B or self.ny <= 2 * self.B:
+        self.H = self.B if halo is None else int(halo)
+        if self.H < self.B:
+            raise ValueError("halo must be at least the stencil border")
+        if self.nx <= 2 * self.H or self.ny <= 2 * self.H:
             raise ValueError("local grid too small for the stencil order")
-        self.gx = self.nx + 2 * self.B
-        self.gy = self.ny + 2 * self.B
+        self.gx = self.nx + 2 * self.H
+        self.gy = self.ny + 2 * self.H
         self.pitch = pitch_for(self.gx)
         self.xcfl = float(np.dtype(np.float32 if dtype == torch.float32 else np.float64).type(params.xcfl))
         self.ycfl = float(np.dtype(np.float32 if dtype == torch.float32 else np.float64).type(params.ycfl))
         self.iteration = 0
         init = torch.full((self.gy, self.pitch), params.ic, dtype=dtype, device=self.device)
         top, left, bottom, right = bc_sides
-        B, ny, nx = self.B, self.ny, self.nx
+        H, ny, nx = self.H, self.ny, self.nx
         # Same write order as the reference: rows first, then columns, so the
         # corners carry the left/right values.
         if bottom:
-            init[:B, :self.gx] = params.bottom_bc
+            init[:H, :self.gx] = params.bottom_bc
         if top:
-            init[B + ny:B + ny + B, :self.gx] = params.top_bc
+            init[H + ny:H + ny + H, :self.gx] = params.top_bc
         if left:
-            init[:, :B] = params.left_bc
+            init[:, :H] = params.left_bc
         if right:
-            init[:, B + nx:B + nx + B] = params.right_bc
+            init[:, H + nx:H + nx + H] = params.right_bc
         self.buf = torch.stack([init, init.clone()])
         self.cur = 0
 
     # -- state --------------------------------------------------------------
     @property
     def interior(self) -> tuple[int, int, int, int]:
-        return (self.B, self.B + self.nx, self.B, self.B + self.ny)
+        return (self.H, self.H + self.nx, self.H, self.H + self.ny)
 
     def curr(self) -> torch.Tensor:
         return self.buf[self.cur]
@@ -80,9 +87,16 @@ class HeatGrid:
     def prev(self) -> torch.Tensor:
         return self.buf[1 - self.cur]
 
+    def view(self, k: int | None = None) -> torch.Tensor:
+        """Device view of state ``k`` (default current) in the reference layout:
+        ``(ny + 2B, nx + 2B)`` -- interior plus a ``border``-deep halo."""
+        k = self.cur if k is None else k
+        o = self.H - self.B
+        return self.buf[k, o:self.gy - o, o:self.gx - o]
+
     def state(self) -> np.ndarray:
-        """Current (gy, gx) grid as a host array."""
-        return self.buf[self.cur, :, :self.gx].cpu().numpy()
+        """Current (ny + 2B, nx + 2B) grid as a host array."""
+        return self.view().cpu().numpy()
 
     # -- compute ------------------------------------------------------------
     def step(self, variant: str = "stream", region=None) -> None:

@@ -33,7 +33,7 @@ import time
 import numpy as np
 import torch
 
-from ..ops.stencil import heat_step
+from ..ops.stencil import heat_step, heat_step2
 from ..parallel.comm import Comm, LoopbackComm, P2P, Pending
 from ..parallel.decomp import Block, decompose
 from ..utils.params import SimParams
@@ -41,42 +41,66 @@ from .heat2d import HeatGrid
 
 
 class _Sub:
-    def __init__(self, blk: Block, grid: HeatGrid):
+    """One subdomain: its block, grid (ghost depth ``H``) and halo views.
+    Every exchange moves ``H``-deep halos: rows straight from/to the grid,
+    columns (and, for ``H > B``, the diagonal corners) via staging."""
+
+    def __init__(self, blk: Block, grid: HeatGrid, corners: bool):
         self.blk = blk
         self.grid = grid
-        B, ny = grid.B, grid.ny
+        H, ny = grid.H, grid.ny
         self.stage = {}
-        if blk.left >= 0 or blk.right >= 0:
-            # contiguous column staging: (B columns x ny rows) per side, send+recv
-            for side in ("left", "right"):
-                if getattr(blk, side) >= 0:
-                    self.stage[side] = (torch.empty((ny, B), dtype=grid.dtype, device=grid.device),
-                                        torch.empty((ny, B), dtype=grid.dtype, device=grid.device))
+        for side in ("left", "right"):
+            if getattr(blk, side) >= 0:
+                self.stage[side] = (torch.empty((ny, H), dtype=grid.dtype, device=grid.device),
+                                    torch.empty((ny, H), dtype=grid.dtype, device=grid.device))
+        self.diag = {}
+        if corners:
+            for dx in (-1, 1):
+                for dy in (-1, 1):
+                    peer = blk.neighbor(dx, dy)
+                    if peer >= 0:
+                        self.diag[(dx, dy)] = peer
+                        self.stage[(dx, dy)] = (torch.empty((H, H), dtype=grid.dtype, device=grid.device),
+                                                torch.empty((H, H), dtype=grid.dtype, device=grid.device))
 
     # views into state k -------------------------------------------------
     def row_send(self, k: int, side: str) -> torch.Tensor:
         g = self.grid
-        B, ny = g.B, g.ny
-        rows = (ny, ny + B) if side == "top" else (B, 2 * B)
+        H, ny = g.H, g.ny
+        rows = (ny, ny + H) if side == "top" else (H, 2 * H)
         return g.buf[k, rows[0]:rows[1]]
 
     def row_recv(self, k: int, side: str) -> torch.Tensor:
         g = self.grid
-        B, ny = g.B, g.ny
-        rows = (ny + B, ny + 2 * B) if side == "top" else (0, B)
+        H, ny = g.H, g.ny
+        rows = (ny + H, ny + 2 * H) if side == "top" else (0, H)
         return g.buf[k, rows[0]:rows[1]]
 
     def col_send_view(self, k: int, side: str) -> torch.Tensor:
         g = self.grid
-        B, nx, ny = g.B, g.nx, g.ny
-        cols = (nx, nx + B) if side == "right" else (B, 2 * B)
-        return g.buf[k, B:B + ny, cols[0]:cols[1]]
+        H, nx, ny = g.H, g.nx, g.ny
+        cols = (nx, nx + H) if side == "right" else (H, 2 * H)
+        return g.buf[k, H:H + ny, cols[0]:cols[1]]
 
     def col_recv_view(self, k: int, side: str) -> torch.Tensor:
         g = self.grid
-        B, nx, ny = g.B, g.nx, g.ny
-        cols = (nx + B, nx + 2 * B) if side == "right" else (0, B)
-        return g.buf[k, B:B + ny, cols[0]:cols[1]]
+        H, nx, ny = g.H, g.nx, g.ny
+        cols = (nx + H, nx + 2 * H) if side == "right" else (0, H)
+        return g.buf[k, H:H + ny, cols[0]:cols[1]]
+
+    def corner_origin(self, dx: int, dy: int, send: bool) -> tuple[int, int]:
+        """(x, y) of the H x H corner block toward diagonal (dx, dy)."""
+        g = self.grid
+        H = g.H
+        if send:
+            return (g.nx if dx > 0 else H), (g.ny if dy > 0 else H)
+        return (g.nx + H if dx > 0 else 0), (g.ny + H if dy > 0 else 0)
+
+    def corner_view(self, k: int, dx: int, dy: int, send: bool) -> torch.Tensor:
+        x, y = self.corner_origin(dx, dy, send)
+        H = self.grid.H
+        return self.grid.buf[k, y:y + H, x:x + H]
 
 
 _OPP = {"top": "bottom", "bottom": "top", "left": "right", "right": "left"}
@@ -88,20 +112,25 @@ class DistHeat:
     subdomains (default: ``comm.size``)."""
 
     def __init__(self, params: SimParams, comm: Comm | None = None, dtype=torch.float32, device="cpu",
-                 local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream"):
+                 local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream",
+                 tblock: int = 1):
         self.p = params
         self.comm = comm or LoopbackComm()
         self.world = world or self.comm.size
         self.local_ranks = local_ranks if local_ranks is not None else [self.comm.rank]
         if self.comm.size > 1 and (len(self.local_ranks) != 1 or self.world != self.comm.size):
             raise ValueError("multi-process runs own exactly one subdomain per rank")
+        if tblock not in (1, 2):
+            raise ValueError("tblock must be 1 or 2")
         self.variant = variant
+        self.tblock = tblock
         self.device = torch.device(device)
         self.subs: dict[int, _Sub] = {}
         for r in self.local_ranks:
             blk = decompose(params.nx, params.ny, self.world, params.grid_method, r)
-            g = HeatGrid(params, dtype, device, nx=blk.nx, ny=blk.ny, bc_sides=blk.bc_sides)
-            self.subs[r] = _Sub(blk, g)
+            g = HeatGrid(params, dtype, device, nx=blk.nx, ny=blk.ny, bc_sides=blk.bc_sides,
+                         halo=tblock * params.border)
+            self.subs[r] = _Sub(blk, g, corners=tblock > 1)
         self.iteration = 0
         # make halos consistent with the neighbours' initial state
         self.exchange(self._cur()).wait()
@@ -137,6 +166,15 @@ class DistHeat:
                     ops.append(P2P("send", sbuf, peer))
                     ops.append(P2P("recv", rbuf, peer))
                     post_unpack.append((s.col_recv_view(k, side), rbuf))
+            for (dx, dy), peer in s.diag.items():
+                if peer in self.subs:
+                    self.subs[peer].corner_view(k, -dx, -dy, False).copy_(s.corner_view(k, dx, dy, True))
+                else:
+                    sbuf, rbuf = s.stage[(dx, dy)]
+                    sbuf.copy_(s.corner_view(k, dx, dy, True))
+                    ops.append(P2P("send", sbuf, peer))
+                    ops.append(P2P("recv", rbuf, peer))
+                    post_unpack.append((s.corner_view(k, dx, dy, False), rbuf))
         pend = self.comm.exchange(ops)
         if not post_unpack:
             return pend
@@ -167,13 +205,13 @@ class DistHeat:
             pend = getattr(self, "_pending", None)
             for s in self.subs.values():
                 g = s.grid
-                for reg in _interior_regions(s):
+                for reg in _interior_regions(s, g.B):
                     heat_step(g.buf[k], g.buf[1 - k], reg, g.order, g.xcfl, g.ycfl, self.variant)
             if pend is not None:
                 pend.wait()
             for s in self.subs.values():
                 g = s.grid
-                for reg in _border_regions(s):
+                for reg in _border_regions(s, g.B):
                     heat_step(g.buf[k], g.buf[1 - k], reg, g.order, g.xcfl, g.ycfl, self.variant)
             self._pending = self.exchange(1 - k)
         for s in self.subs.values():
@@ -181,36 +219,74 @@ class DistHeat:
             s.grid.iteration += 1
         self.iteration += 1
 
+    def step2(self, sync: bool | None = None) -> None:
+        """TWO timesteps per exchange (``tblock=2``): 2B-deep halos (corners
+        included) feed one fused two-step pass per region; the deep interior
+        (2B from any neighbour) overlaps the in-flight exchange in async mode.
+        Same schedule as the native loop (``csrc/hip/dist_heat.hip``)."""
+        if self.tblock != 2:
+            raise ValueError("step2 needs tblock=2 (2B-deep halos)")
+        sync = self.p.sync if sync is None else sync
+        k = self._cur()
+
+        def sweep(regions_of):
+            for s in self.subs.values():
+                g = s.grid
+                ext = _ext_region(s)
+                for reg in regions_of(s, 2 * g.B):
+                    heat_step2(g.buf[k], g.buf[1 - k], reg, ext, g.order, g.xcfl, g.ycfl)
+
+        if sync:
+            sweep(_interior_regions)
+            sweep(_border_regions)
+            self.exchange(1 - k).wait()
+        else:
+            pend = getattr(self, "_pending", None)
+            sweep(_interior_regions)
+            if pend is not None:
+                pend.wait()
+            sweep(_border_regions)
+            self._pending = self.exchange(1 - k)
+        for s in self.subs.values():
+            s.grid.cur = 1 - k
+            s.grid.iteration += 2
+        self.iteration += 2
+
     # -- native loop (RCCL + HIP, no per-step Python) ---------------------
     def _native_plan(self):
         if getattr(self, "_plan", None) is not None:
             return self._plan
-        import numpy as np
-
         (r, s), = self.subs.items()
         g, b = s.grid, s.blk
-        B, ny, pitch = g.B, g.ny, g.pitch
-        interior = [reg for reg in _interior_regions(s)]
-        border = [reg for reg in _border_regions(s)]
+        H, ny, nx, pitch = g.H, g.ny, g.nx, g.pitch
+        D = self.tblock * g.B
+        interior = list(_interior_regions(s, D))
+        border = list(_border_regions(s, D))
         rows, cols = [], []
         for side in ("top", "bottom"):
             peer = getattr(b, side)
             if peer >= 0:
-                send = (ny if side == "top" else B) * pitch
-                recv = (ny + B if side == "top" else 0) * pitch
-                rows.append((peer, send, recv, B * pitch))
+                send = (ny if side == "top" else H) * pitch
+                recv = (ny + H if side == "top" else 0) * pitch
+                rows.append((peer, send, recv, H * pitch))
+        # staged blocks: {peer, send_x, send_y, recv_x, recv_y, rows, width}
         for side in ("left", "right"):
             peer = getattr(b, side)
             if peer >= 0:
-                sx = g.nx if side == "right" else B
-                rx = g.nx + B if side == "right" else 0
-                cols.append((peer, sx, rx, B, ny, B))
-        stage_elems = 2 * sum(c[4] * c[5] for c in cols)
+                sx = nx if side == "right" else H
+                rx = nx + H if side == "right" else 0
+                cols.append((peer, sx, H, rx, H, ny, H))
+        for (dx, dy), peer in s.diag.items():
+            sx, sy = s.corner_origin(dx, dy, True)
+            rx, ry = s.corner_origin(dx, dy, False)
+            cols.append((peer, sx, sy, rx, ry, H, H))
+        stage_elems = 2 * sum(c[5] * c[6] for c in cols)
         plan = {
             "interior": torch.tensor(np.array(interior, dtype=np.int32).reshape(-1, 4)),
             "border": torch.tensor(np.array(border, dtype=np.int32).reshape(-1, 4)),
+            "ext": torch.tensor(np.array(_ext_region(s), dtype=np.int32)),
             "rows": torch.tensor(np.array(rows, dtype=np.int64).reshape(-1, 4)),
-            "cols": torch.tensor(np.array(cols, dtype=np.int32).reshape(-1, 6)),
+            "cols": torch.tensor(np.array(cols, dtype=np.int32).reshape(-1, 7)),
             "stage": torch.empty(max(stage_elems, 1), dtype=g.dtype, device=g.device),
         }
         self._plan = plan
@@ -218,8 +294,9 @@ class DistHeat:
 
     def run_native(self, iters: int, rccl, sync: bool | None = None) -> None:
         """``iters`` timesteps in ONE native call (RCCL P2P halo exchange on a
-        communication stream, interior/exchange overlap in async mode).
-        ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl`."""
+        communication stream, interior/exchange overlap in async mode; with
+        ``tblock=2`` each exchange of 2B-deep halos feeds two timesteps done
+        in one HBM pass). ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl`."""
         import ctypes
 
         from .. import _ext
@@ -234,7 +311,8 @@ class DistHeat:
         cur_out = ctypes.c_int(0)
         _ext.call_hip("cme_heat_dist_run", rccl.handle, g.buf[0].data_ptr(), g.buf[1].data_ptr(), g.pitch, g.gy,
                       plan["interior"].data_ptr(), plan["interior"].shape[0], plan["border"].data_ptr(),
-                      plan["border"].shape[0], plan["rows"].data_ptr(), plan["rows"].shape[0],
+                      plan["border"].shape[0], plan["ext"].data_ptr(), self.tblock,
+                      plan["rows"].data_ptr(), plan["rows"].shape[0],
                       plan["cols"].data_ptr(), plan["cols"].shape[0], plan["stage"].data_ptr(),
                       0 if g.dtype == torch.float32 else 1, g.order, g.xcfl, g.ycfl, iters, g.cur, int(sync), 0,
                       ctypes.addressof(cur_out), _ext.stream_ptr(g.device))
@@ -249,7 +327,12 @@ class DistHeat:
             self._pending = None
 
     def run(self, iters: int, sync: bool | None = None) -> None:
-        for _ in range(iters):
+        i = 0
+        if self.tblock == 2:
+            while i + 1 < iters:
+                self.step2(sync)
+                i += 2
+        for _ in range(i, iters):
             self.step(sync)
         self.finish()
 
@@ -272,27 +355,34 @@ class DistHeat:
         return out
 
 
-def _interior_regions(s: _Sub):
-    """Deep interior: points whose stencil touches no ghost cell that is
-    filled by a neighbour (physical-BC ghosts are constant and always valid)."""
+def _inner_box(s: _Sub, depth: int):
+    """Owned region shrunk by ``depth`` on every side that has a neighbour."""
     g, b = s.grid, s.blk
-    B = g.B
-    xb = 2 * B if b.left >= 0 else B
-    xe = g.nx if b.right >= 0 else B + g.nx
-    yb = 2 * B if b.bottom >= 0 else B
-    ye = g.ny if b.top >= 0 else B + g.ny
+    H = g.H
+    xb = H + depth if b.left >= 0 else H
+    xe = H + g.nx - depth if b.right >= 0 else H + g.nx
+    yb = H + depth if b.bottom >= 0 else H
+    ye = H + g.ny - depth if b.top >= 0 else H + g.ny
+    return xb, xe, yb, ye
+
+
+def _interior_regions(s: _Sub, depth: int):
+    """Deep interior: points whose ``depth``-wide dependency cone (B for one
+    step, 2B for two) touches no ghost cell filled by a neighbour
+    (physical-BC ghosts are constant and always valid)."""
+    xb, xe, yb, ye = _inner_box(s, depth)
     if xe > xb and ye > yb:
         yield (xb, xe, yb, ye)
 
 
-def _border_regions(s: _Sub):
-    g, b = s.grid, s.blk
-    B = g.B
-    xb = 2 * B if b.left >= 0 else B
-    xe = g.nx if b.right >= 0 else B + g.nx
-    yb = 2 * B if b.bottom >= 0 else B
-    ye = g.ny if b.top >= 0 else B + g.ny
-    X0, X1, Y0, Y1 = B, B + g.nx, B, B + g.ny
+def _border_regions(s: _Sub, depth: int):
+    g = s.grid
+    H = g.H
+    xb, xe, yb, ye = _inner_box(s, depth)
+    X0, X1, Y0, Y1 = H, H + g.nx, H, H + g.ny
+    if xe <= xb or ye <= yb:  # subdomain thinner than two cones: one region
+        yield (X0, X1, Y0, Y1)
+        return
     if yb > Y0:
         yield (X0, X1, Y0, yb)  # bottom strip, full width
     if ye < Y1:
@@ -301,6 +391,15 @@ def _border_regions(s: _Sub):
         yield (X0, xb, yb, ye)  # left strip
     if xe < X1:
         yield (xe, X1, yb, ye)  # right strip
+
+
+def _ext_region(s: _Sub):
+    """Region of the intermediate step of a two-step pass: owned region grown
+    by B into the (2B-deep) halo on every neighbour side."""
+    g, b = s.grid, s.blk
+    H, B = g.H, g.B
+    return (H - B if b.left >= 0 else H, H + g.nx + B if b.right >= 0 else H + g.nx,
+            H - B if b.bottom >= 0 else H, H + g.ny + B if b.top >= 0 else H + g.ny)
 
 
 def run_hw5(params_path: str, comm: Comm | None = None, dtype=torch.float64, device: str | None = None,

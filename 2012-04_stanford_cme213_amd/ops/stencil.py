@@ -18,7 +18,9 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiipp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipipipiiddiiiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiippiffip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiippiddip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipipipipiiddiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -58,6 +60,27 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
     else:
         name = "cme_cpu_heat_step_f64" if f64 else "cme_cpu_heat_step_f32"
         _ext.call_cpu(name, prev.data_ptr(), curr.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl)
+
+
+def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, int, int],
+               ext: tuple[int, int, int, int], order: int, xcfl: float, ycfl: float, chunk: int = 0) -> None:
+    """TWO timesteps in one HBM pass (GPU only): the intermediate step covers
+    ``ext`` (``region`` grown by at most B cells, e.g. into a 2B-deep halo),
+    the second writes ``curr[region]``. Cells of ``ext`` outside the grid's
+    update set keep their value. Equal, bit for bit, to two single steps on
+    (ext, then region). On CPU it runs exactly that (through a temporary)."""
+    _check(prev, curr)
+    if not prev.is_cuda:
+        tmp = prev.clone()
+        heat_step(prev, tmp, ext, order, xcfl, ycfl)
+        heat_step(tmp, curr, region, order, xcfl, ycfl)
+        return
+    rows, pitch = prev.shape
+    r = (ctypes.c_int * 4)(*map(int, region))
+    e = (ctypes.c_int * 4)(*map(int, ext))
+    name = "cme_heat_step2_f64" if prev.dtype == torch.float64 else "cme_heat_step2_f32"
+    _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), ctypes.addressof(e),
+                  order, xcfl, ycfl, chunk, _ext.stream_ptr(prev.device))
 
 
 def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,

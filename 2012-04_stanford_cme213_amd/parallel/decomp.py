@@ -48,6 +48,15 @@ class Block:
     top: int = -1
     bottom: int = -1
 
+    def neighbor(self, dx: int, dy: int) -> int:
+        """Rank of the block at (col + dx, row + dy), or -1 outside the grid
+        (dy = +1 is "top"). Diagonal peers feed the corner halos that
+        temporal blocking needs."""
+        c, r = self.col + dx, self.row + dy
+        if 0 <= c < self.px and 0 <= r < self.py:
+            return r * self.px + c
+        return -1
+
     @property
     def bc_sides(self) -> tuple[bool, bool, bool, bool]:
         """(top, left, bottom, right): True where the physical BC applies."""

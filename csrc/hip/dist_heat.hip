@@ -21,6 +21,10 @@ extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int 
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream);
 extern "C" int cme_heat_step_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, double xcfl, double ycfl, int chunk, void* stream);
+extern "C" int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
+                                  int order, float xcfl, float ycfl, int chunk, void* stream);
+extern "C" int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
+                                  int order, double xcfl, double ycfl, int chunk, void* stream);
 
 #define CME_TRY_INT(expr)                 \
     do {                                  \
@@ -111,9 +115,11 @@ CME_EXPORT int cme_rccl_p2p(void* comm, int n, const int* peers, const int* is_s
 
 namespace {
 
+// Staged rectangular blocks (column halos, corner halos): rows x w elements
+// at (x0, y0) <-> contiguous staging.
 template <typename T>
-__global__ __launch_bounds__(256) void pack_cols_kernel(const T* __restrict__ g, int pitch, int x0, int y0, int ny,
-                                                        int w, T* __restrict__ stage) {
+__global__ __launch_bounds__(256) void pack_block_kernel(const T* __restrict__ g, int pitch, int x0, int y0, int ny,
+                                                         int w, T* __restrict__ stage) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= ny * w) return;
     const int r = i / w, c = i % w;
@@ -121,8 +127,8 @@ __global__ __launch_bounds__(256) void pack_cols_kernel(const T* __restrict__ g,
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void unpack_cols_kernel(T* __restrict__ g, int pitch, int x0, int y0, int ny, int w,
-                                                          const T* __restrict__ stage) {
+__global__ __launch_bounds__(256) void unpack_block_kernel(T* __restrict__ g, int pitch, int x0, int y0, int ny, int w,
+                                                           const T* __restrict__ stage) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= ny * w) return;
     const int r = i / w, c = i % w;
@@ -164,21 +170,42 @@ int step_region<double>(const double* p, double* c, int pitch, int gy, const int
     return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, 2, xcfl, ycfl, 0, (void*)s);
 }
 
-// Exchange plan for buffer `g`:
-//   rows[i*4 + 0..3]  = {peer, send_off, recv_off, count}  (element offsets)
-//   cols[i*6 + 0..5]  = {peer, send_x, recv_x, y0, ny, width}
-//   stage: 2 * sum(ny*width) elements (send halves first, then recv halves)
 template <typename T>
-int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n_rows, const int* cols, int n_cols,
+int step2_region(const T* p, T* c, int pitch, int gy, const int* r, const int* ext, int order, T xcfl, T ycfl,
+                 hipStream_t s);
+
+template <>
+int step2_region<float>(const float* p, float* c, int pitch, int gy, const int* r, const int* ext, int order,
+                        float xcfl, float ycfl, hipStream_t s) {
+    return cme_heat_step2_f32(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, (void*)s);
+}
+template <>
+int step2_region<double>(const double* p, double* c, int pitch, int gy, const int* r, const int* ext, int order,
+                         double xcfl, double ycfl, hipStream_t s) {
+    return cme_heat_step2_f64(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, (void*)s);
+}
+
+// Exchange plan for buffer `g`:
+//   rows[i*4 + 0..3]  = {peer, send_off, recv_off, count}  (element offsets;
+//                       full pitched rows go straight out of / into the grid)
+//   blks[i*7 + 0..6]  = {peer, send_x, send_y, recv_x, recv_y, rows, width}
+//                       (column halos and, for 2B-deep halos, the corners
+//                       to/from the diagonal peers)
+//   stage: 2 * sum(rows*width) elements (send halves first, then recv halves)
+constexpr int kBlk = 7;
+
+template <typename T>
+int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n_rows, const int* blks, int n_blks,
                   T* stage, ncclDataType_t dt, hipStream_t cs) {
-    long long stage_send = 0, total = 0;
-    for (int i = 0; i < n_cols; ++i) total += (long long)cols[i * 6 + 4] * cols[i * 6 + 5];
-    for (int i = 0; i < n_cols; ++i) {
-        const int* c = cols + i * 6;
-        const int cnt = c[4] * c[5];
-        hipLaunchKernelGGL(pack_cols_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[1], c[3], c[4],
-                           c[5], stage + stage_send);
-        stage_send += cnt;
+    long long total = 0;
+    for (int i = 0; i < n_blks; ++i) total += (long long)blks[i * kBlk + 5] * blks[i * kBlk + 6];
+    long long off = 0;
+    for (int i = 0; i < n_blks; ++i) {
+        const int* c = blks + i * kBlk;
+        const int cnt = c[5] * c[6];
+        hipLaunchKernelGGL(pack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[1], c[2], c[5],
+                           c[6], stage + off);
+        off += cnt;
     }
     CME_TRY(hipGetLastError());
     NCCL_TRY(ncclGroupStart());
@@ -187,21 +214,21 @@ int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n
         NCCL_TRY(ncclSend(g + r[1], (size_t)r[3], dt, (int)r[0], comm, cs));
         NCCL_TRY(ncclRecv(g + r[2], (size_t)r[3], dt, (int)r[0], comm, cs));
     }
-    long long off = 0;
-    for (int i = 0; i < n_cols; ++i) {
-        const int* c = cols + i * 6;
-        const long long cnt = (long long)c[4] * c[5];
+    off = 0;
+    for (int i = 0; i < n_blks; ++i) {
+        const int* c = blks + i * kBlk;
+        const long long cnt = (long long)c[5] * c[6];
         NCCL_TRY(ncclSend(stage + off, (size_t)cnt, dt, c[0], comm, cs));
         NCCL_TRY(ncclRecv(stage + total + off, (size_t)cnt, dt, c[0], comm, cs));
         off += cnt;
     }
     NCCL_TRY(ncclGroupEnd());
     off = 0;
-    for (int i = 0; i < n_cols; ++i) {
-        const int* c = cols + i * 6;
-        const int cnt = c[4] * c[5];
-        hipLaunchKernelGGL(unpack_cols_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[2], c[3], c[4],
-                           c[5], stage + total + off);
+    for (int i = 0; i < n_blks; ++i) {
+        const int* c = blks + i * kBlk;
+        const int cnt = c[5] * c[6];
+        hipLaunchKernelGGL(unpack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[3], c[4], c[5],
+                           c[6], stage + total + off);
         off += cnt;
     }
     CME_TRY(hipGetLastError());
@@ -210,7 +237,7 @@ int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n
 
 template <typename T>
 int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* interior, int n_int, const int* border,
-             int n_b, const long long* rows, int n_rows, const int* cols, int n_cols, T* stage, int order, T xcfl,
+             int n_b, const int* ext, int tblock, const long long* rows, int n_rows, const int* cols, int n_cols, T* stage, int order, T xcfl,
              T ycfl, int iters, int cur, int sync, int exchange_first, int* cur_out, hipStream_t s) {
     DistCtx* ctx;
     CME_TRY_INT(get_ctx(&ctx));
@@ -225,12 +252,24 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
         CME_TRY(hipEventRecord(ctx->ev_comm, cs));
         CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
     }
-    for (int it = 0; it < iters; ++it) {
+    // tblock == 2: halos are 2B deep, each exchange feeds TWO timesteps computed
+    // in one pass (stream2, intermediate step on region `ext`); odd tails
+    // take one single step (the 2B halo over-satisfies it).
+    for (int it = 0; it < iters;) {
         const T* p = bufs[cur];
         T* c = bufs[cur ^ 1];
+        const bool two = tblock == 2 && it + 1 < iters;
+        auto sweep = [&](const int* regs, int n) -> int {
+            for (int i = 0; i < n; ++i) {
+                int rc = two ? step2_region<T>(p, c, pitch, gy, regs + 4 * i, ext, order, xcfl, ycfl, s)
+                             : step_region<T>(p, c, pitch, gy, regs + 4 * i, order, xcfl, ycfl, s);
+                if (rc) return rc;
+            }
+            return 0;
+        };
         if (sync) {
-            for (int i = 0; i < n_int; ++i) CME_TRY_INT(step_region<T>(p, c, pitch, gy, interior + 4 * i, order, xcfl, ycfl, s));
-            for (int i = 0; i < n_b; ++i) CME_TRY_INT(step_region<T>(p, c, pitch, gy, border + 4 * i, order, xcfl, ycfl, s));
+            CME_TRY_INT(sweep(interior, n_int));
+            CME_TRY_INT(sweep(border, n_b));
             CME_TRY(hipEventRecord(ctx->ev_compute, s));
             CME_TRY(hipStreamWaitEvent(cs, ctx->ev_compute, 0));
             int rc = post_exchange<T>(comm, c, pitch, rows, n_rows, cols, n_cols, stage, dt, cs);
@@ -239,9 +278,9 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
             CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
         } else {
             // deep interior needs no ghost cells: overlaps the previous exchange
-            for (int i = 0; i < n_int; ++i) CME_TRY_INT(step_region<T>(p, c, pitch, gy, interior + 4 * i, order, xcfl, ycfl, s));
+            CME_TRY_INT(sweep(interior, n_int));
             CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));  // halos of p have arrived
-            for (int i = 0; i < n_b; ++i) CME_TRY_INT(step_region<T>(p, c, pitch, gy, border + 4 * i, order, xcfl, ycfl, s));
+            CME_TRY_INT(sweep(border, n_b));
             CME_TRY(hipEventRecord(ctx->ev_compute, s));
             CME_TRY(hipStreamWaitEvent(cs, ctx->ev_compute, 0));
             int rc = post_exchange<T>(comm, c, pitch, rows, n_rows, cols, n_cols, stage, dt, cs);
@@ -249,6 +288,7 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
             CME_TRY(hipEventRecord(ctx->ev_comm, cs));
         }
         cur ^= 1;
+        it += two ? 2 : 1;
     }
     // leave the compute stream ordered after the last exchange
     CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
@@ -259,15 +299,18 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
 }  // namespace
 
 // The distributed heat loop (see dist_run). dtype 0 = f32, 1 = f64.
+// tblock 1: one step per exchange; 2: two steps per exchange (needs 2B-deep
+// halos, `interior` shrunk by 2B on neighbour sides, `ext` = owned region
+// grown by B on neighbour sides).
 CME_EXPORT int cme_heat_dist_run(void* comm, void* buf0, void* buf1, int pitch, int gy, const int* interior, int n_int,
-                                 const int* border, int n_b, const long long* rows, int n_rows, const int* cols,
+                                 const int* border, int n_b, const int* ext, int tblock, const long long* rows, int n_rows, const int* cols,
                                  int n_cols, void* stage, int dtype, int order, double xcfl, double ycfl, int iters,
                                  int cur, int sync, int exchange_first, int* cur_out, void* stream) {
     if (dtype == 0)
         return dist_run<float>((ncclComm_t)comm, (float*)buf0, (float*)buf1, pitch, gy, interior, n_int, border, n_b,
-                               rows, n_rows, cols, n_cols, (float*)stage, order, (float)xcfl, (float)ycfl, iters, cur,
+                               ext, tblock, rows, n_rows, cols, n_cols, (float*)stage, order, (float)xcfl, (float)ycfl, iters, cur,
                                sync, exchange_first, cur_out, as_stream(stream));
     return dist_run<double>((ncclComm_t)comm, (double*)buf0, (double*)buf1, pitch, gy, interior, n_int, border, n_b,
-                            rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
+                            ext, tblock, rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
                             exchange_first, cur_out, as_stream(stream));
 }

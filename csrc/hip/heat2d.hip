@@ -193,8 +193,9 @@ constexpr int kStrip2Out = 60 * 4;
 
 template <typename T, int ORDER, int RB>
 __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
-                                                           int gy, int xb, int xe, int yb, int ye, int strips,
-                                                           int chunk, int total_waves, T xcfl, T ycfl) {
+                                                           int gy, int xb, int xe, int yb, int ye, int xb1,
+                                                           int xe1, int yb1, int ye1, int strips, int chunk,
+                                                           int total_waves, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
     constexpr int NW = RB + 2 * B;
     const int lane = lane_id();
@@ -216,8 +217,8 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
         return src + (size_t)r * pitch;
     };
     // one FTCS update of the 4 columns of this lane for a row whose window is
-    // w[k0 .. k0+2B]; cells outside the region keep their value
-    auto update = [&](const V4<T>* w, int k0, int row) -> V4<T> {
+    // w[k0 .. k0+2B]; cells outside region [rxb,rxe)x[ryb,rye) keep their value
+    auto update = [&](const V4<T>* w, int k0, int row, int rxb, int rxe, int ryb, int rye) -> V4<T> {
         const V4<T> c = w[k0 + B];
         const V4<T> L = wave_shr1(c);
         const V4<T> R = wave_shl1(c);
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
             rowv[8 + j] = R[j];
         }
         V4<T> o;
-        const bool row_in = row >= yb && row < ye;
+        const bool row_in = row >= ryb && row < rye;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             T xm[B], xp[B], ym[B], yp[B];
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
             }
             const T u = heat_update<ORDER>(c[j], xm, xp, ym, yp, xcfl, ycfl);
             const int x = xbase + j;
-            o[j] = (row_in && x >= xb && x < xe) ? u : c[j];
+            o[j] = (row_in && x >= rxb && x < rxe) ? u : c[j];
         }
         return o;
     };
@@ -263,11 +264,11 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
             for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
         }
 #pragma unroll
-        for (int i = 0; i < RB; ++i) s1[2 * B + i] = update(in, i, r0 + i);
+        for (int i = 0; i < RB; ++i) s1[2 * B + i] = update(in, i, r0 + i, xb1, xe1, yb1, ye1);
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
             const int y = r0 - B + i;
-            const V4<T> o = update(s1, i, y);
+            const V4<T> o = update(s1, i, y, xb, xe, yb, ye);
             if (out_lane && y >= y0 && y < y1) {
                 T* d = dst + (size_t)y * pitch;
                 if (full_vec) {
@@ -288,11 +289,40 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
 }
 
 // ---------------------------------------------------------------- launchers
-namespace {
-
 struct Region {
     int xb, xe, yb, ye;
 };
+
+// Two-step pass: output region `g`; step-1 (intermediate) region `g1` must
+// contain g and may extend at most B cells beyond it (into a 2B-deep halo,
+// for the distributed loop); cells outside g1 keep their input value.
+template <typename T, int ORDER>
+int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
+                   hipStream_t s) {
+    constexpr int RB = sizeof(T) == 4 ? 4 : 2;
+    const int H = g.ye - g.yb;
+    if (H <= 0 || g.xe <= g.xb) return 0;
+    const int x_lo = g.xb & ~3;
+    const int strips = (int)cdiv(g.xe - x_lo, kStrip2Out);
+    int chunk = chunk_hint;
+    if (chunk <= 0) {
+        const long target_waves = 256L * 12;
+        long rows = ((long)strips * H + target_waves - 1) / target_waves;
+        rows = rows < 4 * RB ? 4 * RB : rows;
+        rows = rows > 512 ? 512 : rows;
+        chunk = (int)rows;
+    }
+    chunk = ((chunk + RB - 1) / RB) * RB;
+    const int chunks = (int)cdiv(H, chunk);
+    const int total_waves = strips * chunks;
+    hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
+                       pitch, gy, g.xb, g.xe, g.yb, g.ye, g1.xb, g1.xe, g1.yb, g1.ye, strips, chunk, total_waves, xcfl,
+                       ycfl);
+    CME_LAUNCH_STATUS();
+}
+
+namespace {
+
 
 template <typename T, int ORDER>
 int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, int chunk_hint,
@@ -310,23 +340,8 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         hipLaunchKernelGGL((heat_lds_kernel<T, ORDER, TY, 1>), grid, dim3(256), 0, s, prev, curr, pitch, gy, g.xb,
                            g.xe, g.yb, g.ye, xcfl, ycfl);
     } else if (variant == 4) {
-        // TWO timesteps per launch (temporal blocking)
-        constexpr int RB = sizeof(T) == 4 ? 4 : 2;
-        const int x_lo = g.xb & ~3;
-        const int strips = (int)cdiv(g.xe - x_lo, kStrip2Out);
-        int chunk = chunk_hint;
-        if (chunk <= 0) {
-            const long target_waves = 256L * 12;
-            long rows = ((long)strips * H + target_waves - 1) / target_waves;
-            rows = rows < 4 * RB ? 4 * RB : rows;
-            rows = rows > 512 ? 512 : rows;
-            chunk = (int)rows;
-        }
-        chunk = ((chunk + RB - 1) / RB) * RB;
-        const int chunks = (int)cdiv(H, chunk);
-        const int total_waves = strips * chunks;
-        hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev,
-                           curr, pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
+        // TWO timesteps per launch (temporal blocking), step-1 region = output
+        return launch_stream2<T, ORDER>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s);
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -366,7 +381,32 @@ int dispatch_heat(int order, int variant, const T* prev, T* curr, int pitch, int
     }
 }
 
+template <typename T>
+int dispatch_stream2(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
+                     int chunk, hipStream_t s) {
+    switch (order) {
+        case 2: return launch_stream2<T, 2>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 4: return launch_stream2<T, 4>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 8: return launch_stream2<T, 8>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
 }  // namespace
+
+// TWO timesteps in one pass: curr[out] = FTCS^2(prev) where the intermediate
+// step is applied on region `ext` (out grown by <= B cells into a halo).
+CME_EXPORT int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
+                                  int order, float xcfl, float ycfl, int chunk, void* stream) {
+    return dispatch_stream2<float>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
+                                   Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, as_stream(stream));
+}
+
+CME_EXPORT int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
+                                  int order, double xcfl, double ycfl, int chunk, void* stream) {
+    return dispatch_stream2<double>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
+                                    Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, as_stream(stream));
+}
 
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO steps)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,

@@ -7,7 +7,7 @@ import torch
 from dist_util import run_ranks
 
 
-def _heat_rank(rank, world, method, sync, order):
+def _heat_rank(rank, world, method, sync, order, tblock=1):
     import cme213x
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.parallel.comm import TorchComm
@@ -15,11 +15,11 @@ def _heat_rank(rank, world, method, sync, order):
 
     p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   sync=sync, flavor="hw5")
-    sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive")
+    sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive", tblock=tblock)
     # non-uniform initial condition (same on every rank, by global coords)
     for s in sim.subs.values():
         g, b = s.grid, s.blk
-        B = g.B
+        B = g.H
         yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
         ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0)
         g.buf[:, B:B + b.ny, B:B + b.nx] = ic
@@ -46,13 +46,44 @@ def _single(method, order, sync):
     return g.state()[B:-B, B:-B]
 
 
-@pytest.mark.parametrize("method,sync,order,world", [(1, True, 8, 2), (1, False, 4, 2), (2, False, 8, 4),
-                                                     (2, True, 2, 4)])
-def test_dist_heat_matches_single(method, sync, order, world):
-    parts = run_ranks(_heat_rank, world, (method, sync, order))
+@pytest.mark.parametrize("method,sync,order,world,tblock",
+                         [(1, True, 8, 2, 1), (1, False, 4, 2, 1), (2, False, 8, 4, 1), (2, True, 2, 4, 1),
+                          (1, False, 8, 3, 2), (1, True, 4, 2, 2), (2, False, 8, 4, 2), (2, True, 2, 4, 2),
+                          (2, False, 4, 6, 2)])
+def test_dist_heat_matches_single(method, sync, order, world, tblock):
+    parts = run_ranks(_heat_rank, world, (method, sync, order, tblock))
     ref = _single(method, order, sync)
     for x0, y0, st in parts:
         np.testing.assert_array_equal(st, ref[y0:y0 + st.shape[0], x0:x0 + st.shape[1]])
+
+
+@pytest.mark.parametrize("method,world", [(1, 3), (2, 4), (2, 6)])
+def test_deep_halo_exchange_fills_corners(method, world):
+    """With 2B-deep halos every ghost cell of a subdomain (corners included)
+    must hold the neighbouring owner's value after one exchange."""
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=61, ny=47, order=4, ic=0.0, bc=(-1.0, -2.0, -3.0, -4.0), grid_method=method, flavor="hw5")
+    sim = DistHeat(p, None, torch.float64, "cpu", local_ranks=list(range(world)), world=world, tblock=2)
+    f = lambda y, x: 1000.0 * y + x  # noqa: E731  global field by global coords
+    for s in sim.subs.values():
+        g, b = s.grid, s.blk
+        H = g.H
+        yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+        g.buf[g.cur, H:H + b.ny, H:H + b.nx] = torch.from_numpy(f(yy, xx))
+    sim.exchange(sim._cur()).wait()
+    for s in sim.subs.values():
+        g, b = s.grid, s.blk
+        H = g.H
+        st = g.buf[g.cur, :g.gy, :g.gx].numpy()
+        gy_ = np.arange(g.gy) - H + b.y0
+        gx_ = np.arange(g.gx) - H + b.x0
+        inside_y = (gy_ >= 0) & (gy_ < p.ny)
+        inside_x = (gx_ >= 0) & (gx_ < p.nx)
+        m = np.outer(inside_y, inside_x)
+        yy, xx = np.meshgrid(gy_, gx_, indexing="ij")
+        np.testing.assert_array_equal(st[m], f(yy, xx)[m])
 
 
 def _collectives(rank, world):

@@ -22,7 +22,8 @@ def _setup_single():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sync", [True, False])
-def test_native_loop_world1(gpu, sync):
+@pytest.mark.parametrize("tblock", [1, 2])
+def test_native_loop_world1(gpu, sync, tblock):
     import torch.distributed as dist
 
     from cme213x.models.heat2d import HeatGrid
@@ -32,13 +33,13 @@ def test_native_loop_world1(gpu, sync):
     from cme213x.utils.params import SimParams
 
     _setup_single()
-    p = SimParams(nx=300, ny=211, order=8, iters=6, sync=sync, flavor="hw5")
-    sim = DistHeat(p, TorchComm(), torch.float32, gpu)
+    p = SimParams(nx=300, ny=211, order=8, iters=7, sync=sync, flavor="hw5")
+    sim = DistHeat(p, TorchComm(), torch.float32, gpu, tblock=tblock)
     rc = NativeRccl()
-    sim.run_native(6, rc)
+    sim.run_native(7, rc)
     torch.cuda.synchronize()
     ref = HeatGrid(p, torch.float32, gpu)
-    ref.run(6, "stream")
+    ref.run(7, "stream")
     B = p.border
     assert np.array_equal(sim.gather_global()[B:-B, B:-B], ref.state().astype(np.float64)[B:-B, B:-B])
     x = torch.arange(10, dtype=torch.float32, device=gpu)
@@ -46,6 +47,35 @@ def test_native_loop_world1(gpu, sync):
     assert torch.equal(x.cpu(), torch.arange(10, dtype=torch.float32))
     rc.close()
     dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,world,sync", [(1, 4, False), (2, 4, False), (2, 6, True), (1, 3, True)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype):
+    """Several subdomains in one process on the GPU (halo exchange = device
+    copies): the fused two-step kernel on interior/border regions with the
+    step-1 region grown into 2B-deep halos must reproduce the single-grid CPU
+    oracle bit for bit."""
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=333, ny=270, order=8, iters=7, sync=sync, grid_method=method, ic=5.0,
+                  bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
+    ref = DistHeat(p, None, dtype, "cpu", variant="naive")
+    sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=2)
+    for d in (ref, sim):
+        for s in d.subs.values():
+            g, b = s.grid, s.blk
+            H = g.H
+            yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+            ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0).to(dtype)
+            g.buf[:, H:H + b.ny, H:H + b.nx] = ic.to(g.device)
+        d.exchange(d._cur()).wait()
+    ref.run(p.iters)
+    sim.run(p.iters)
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
 
 
 def _two_ranks_same_gpu(rank, world, method, sync, native):
