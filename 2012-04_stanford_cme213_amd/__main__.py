@@ -1,7 +1,7 @@
 """``python -m cme213x <command> [args]`` -- the reference's programs."""
 import sys
 
-from .drivers import final, hw1, hw2_hw5, hw3, hw4
+from .drivers import final, hw1, hw2_hw5, hw3, hw4, studies
 
 COMMANDS = {
     "cipher": hw1.cipher_main,
@@ -16,6 +16,8 @@ COMMANDS = {
     "checker": final.checker_main,
     "readmm": final.readmm_main,
     "genfp": final.genfp_main,
+    "occupancy": studies.occupancy_main,
+    "study": studies.study_main,
 }
 
 

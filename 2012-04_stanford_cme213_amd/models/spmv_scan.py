@@ -25,6 +25,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from .. import _ext
 from ..ops.scan import head_flags_from_offsets, segmented_scan, spmv_scan_run
 from ..utils.gridio import write_vector
 from ..utils.timer import EventTimer
@@ -110,12 +111,29 @@ REF_MS = {"cant": 107.911, "consph": 62.117, "cop20k_A": 146.603, "dense2": 26.6
           "rail4284": 58.752, "rma10": 99.947, "scircuit": 47.816, "shipsec1": 42.401, "webbase-1M": 592.115}
 
 
-class SpmvScanSolver:
-    """Device-resident state: a (updated in place), xx = x[k], head bitmask."""
+_ext.proto(_ext.HIP_PROTOS, "cme_segscan_offsets_run", "pppiiip")
 
-    def __init__(self, prob: SpmvScanProblem, device="cuda"):
+ALGOS = ("lookback", "wave", "serial")
+
+
+class SpmvScanSolver:
+    """Device-resident state: a (updated in place), xx = x[k], head bitmask.
+
+    ``algo``: "lookback" (default; single-pass decoupled look-back segmented
+    scan over the whole array, load-balanced whatever the segment lengths),
+    "wave" (one wave per segment: the reference's ``fp.cu`` algorithm, made
+    race-free with a DPP scan), "serial" (one lane per segment: ``fp_old.cu``).
+    The last two are GPU-only comparison variants."""
+
+    def __init__(self, prob: SpmvScanProblem, device="cuda", algo: str = "lookback"):
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {ALGOS}")
         self.prob = prob
+        self.algo = algo
         self.device = torch.device(device)
+        if algo != "lookback" and self.device.type != "cuda":
+            raise ValueError(f"algo {algo!r} is a GPU kernel")
+        self.offsets = torch.from_numpy(prob.s.astype(np.int32)).to(self.device)
         x = torch.from_numpy(prob.x).to(self.device)
         k = torch.from_numpy(prob.k.astype(np.int64)).to(self.device)
         self.xx = x[k].contiguous()  # pre-flattened gather (untimed, fp.cu:124-125)
@@ -126,10 +144,18 @@ class SpmvScanSolver:
         self.a.copy_(torch.from_numpy(self.prob.a))
 
     def step(self) -> None:
+        if self.algo != "lookback":
+            self.run(1)
+            return
         segmented_scan(self.a, self.flags, out=self.a, mul=self.xx)
 
     def run(self, iters: int | None = None) -> torch.Tensor:
-        return spmv_scan_run(self.a, self.xx, self.flags, self.prob.iters if iters is None else iters)
+        iters = self.prob.iters if iters is None else iters
+        if self.algo == "lookback":
+            return spmv_scan_run(self.a, self.xx, self.flags, iters)
+        _ext.call_hip("cme_segscan_offsets_run", self.a.data_ptr(), self.xx.data_ptr(), self.offsets.data_ptr(),
+                      self.prob.p - 1, 0 if self.algo == "serial" else 1, iters, _ext.stream_ptr(self.device))
+        return self.a
 
 
 def reference_solution(prob: SpmvScanProblem, iters: int | None = None) -> np.ndarray:
@@ -161,12 +187,12 @@ def errors(ref: np.ndarray, b: np.ndarray) -> dict:
 
 
 def run_fp(a_path: str, x_path: str, cpu_check: bool = False, device: str | None = None,
-           out_path: str = "b.txt") -> dict:
+           out_path: str = "b.txt", algo: str = "lookback") -> dict:
     """The ``./fp a.txt x.txt [check]`` driver (``fp.cu:74-216``)."""
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
     prob = load(a_path, x_path)
     print(f"\nDim of a: {prob.n}\nDim of x: {prob.q}\nDim of s: {prob.p}\n# of iters: {prob.iters}\n")
-    sol = SpmvScanSolver(prob, device)
+    sol = SpmvScanSolver(prob, device, algo)
     sol.run(1)  # warm-up (code object load), then restore a
     sol.reset()
     t = EventTimer("spmv-scan", device=device if device != "cpu" else None, print_result=False)

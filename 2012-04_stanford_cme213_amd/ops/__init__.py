@@ -1,1 +1,1 @@
-from . import stencil, elementwise, graph, scan, transpose, spmv, sort, text, gemm, atomics  # noqa: F401
+from . import stencil, elementwise, graph, scan, transpose, spmv, sort, text, gemm, atomics, algorithms, studies  # noqa: F401

@@ -52,11 +52,14 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     return t
 
 
-def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "radix", num_bits: int = 8):
+def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "radix", num_bits: int = 8,
+         key_bits: int = 32):
     """Sort a 1-D tensor (optionally carrying int32/uint32/float32 values).
     GPU algos: "radix" (stable), "merge". CPU algos: "radix" (OpenMP,
     ``num_bits`` per pass), "radix_serial", "merge" (OpenMP tasks, keys only).
-    Returns sorted keys (and values)."""
+    ``key_bits`` < 32 (GPU radix, non-negative integer keys below
+    ``2**key_bits``) runs only the passes covering those bits -- a counting
+    sort when ``key_bits <= 8``. Returns sorted keys (and values)."""
     if keys.dim() != 1:
         raise ValueError("1-D keys expected")
     n = keys.numel()
@@ -73,7 +76,16 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
         v2p = v2.data_ptr() if v2 is not None else None
         if algo == "radix":
             ws = _workspace(keys.device, 2 * 1024 * 256 * 4 + 65536)
-            _ext.call_hip("cme_radix_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, 0, 32, ws.data_ptr(), s)
+            if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
+                raise TypeError("key_bits < 32 needs non-negative integer keys")
+            bits = 32 if key_bits >= 32 else max(1, int(key_bits))
+            if key_bits < 32 and dtype == torch.int32:
+                k = keys.contiguous().clone().view(torch.uint32)  # no sign flip: keys are non-negative
+                k2 = torch.empty_like(k)
+            _ext.call_hip("cme_radix_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, 0, bits, ws.data_ptr(), s)
+            if key_bits < 32 and dtype == torch.int32:
+                out = k.view(torch.int32)
+                return (out, v.view(values.dtype)) if values is not None else out
         elif algo == "merge":
             _ext.call_hip("cme_merge_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, s)
         else:

@@ -1,1 +1,1 @@
-from . import params, ulp, timer, gridio, mmio  # noqa: F401
+from . import params, ulp, timer, gridio, mmio, occupancy  # noqa: F401

@@ -93,6 +93,23 @@ def main():
             emit(bench="spmvscan", matrix=name, n=n, p=p, N=N, ms=ms, GBps=12 * n * N / ms / 1e6,
                  ref_ms=REF_MS[name], speedup_vs_ref=REF_MS[name] / ms)
 
+    if want("spmvscan_algos"):
+        from cme213x.models.spmv_scan import BENCH_SHAPES, REF_MS, SpmvScanSolver, generate
+
+        for name in ("dense2", "mac_econ_fwd500", "webbase-1M", "mc2depi"):
+            n, p, N = BENCH_SHAPES[name]
+            prob = generate(n, p, 100000, N, seed=1)
+            for algo in ("lookback", "wave", "serial"):
+                sol = SpmvScanSolver(prob, dev, algo)
+                sol.run(1)
+                ms = timeit(lambda: sol.run(), iters=3, warmup=1)
+                emit(bench="spmvscan_algo", matrix=name, algo=algo, n=n, p=p, N=N, ms=ms,
+                     GBps=12 * n * N / ms / 1e6, ref_ms=REF_MS[name], speedup_vs_ref=REF_MS[name] / ms)
+                del sol
+
+    if want("algorithms"):
+        bench_algorithms(emit, timeit)
+
     if want("cipher"):
         path = "/root/reference/hw/hw1/programming/mobydick.txt"
         text = np.fromfile(path, dtype=np.uint8) if os.path.exists(path) else \
@@ -239,6 +256,43 @@ def bench_gemm(emit, timeit):
         torch.backends.cuda.matmul.allow_tf32 = False
         ms = timeit(lambda: torch.mm(A, B, out=C), iters=3, warmup=1)
         emit(bench="sgemm", n=n, variant="torch.mm(hipBLASLt)", ms=ms, GFLOPs=2 * n ** 3 / ms / 1e6)
+
+
+def bench_algorithms(emit, timeit):
+    import torch
+
+    from cme213x.ops import algorithms as A
+
+    n = 1 << 26
+    x = torch.rand(n, device="cuda")
+    m = x < 0.5
+    ms = timeit(lambda: A.copy_if(x, m))
+    emit(bench="copy_if", n=n, ms=ms, GBps=(4 * n + 2 * n + 4 * n / 2) / ms / 1e6)
+    ms = timeit(lambda: x[m])
+    emit(bench="copy_if", impl="torch x[mask]", n=n, ms=ms, GBps=(4 * n + 2 * n + 4 * n / 2) / ms / 1e6)
+    ms = timeit(lambda: A.stable_partition(x, m))
+    emit(bench="stable_partition", n=n, ms=ms, GBps=(8 * n + 2 * n) / ms / 1e6)
+    k = torch.sort(torch.randint(0, 1 << 20, (n,), device="cuda", dtype=torch.int32)).values
+    ms = timeit(lambda: A.unique(k))
+    emit(bench="unique", n=n, ms=ms, GBps=(4 * n + 4 * (1 << 20)) / ms / 1e6)
+    ms = timeit(lambda: torch.unique_consecutive(k))
+    emit(bench="unique", impl="torch.unique_consecutive", n=n, ms=ms, GBps=(4 * n + 4 * (1 << 20)) / ms / 1e6)
+    v = torch.rand(n, device="cuda")
+    ms = timeit(lambda: A.reduce_by_key(k, v))
+    emit(bench="reduce_by_key", n=n, segments=1 << 20, ms=ms)
+    q = torch.randint(0, 1 << 20, (1 << 24,), device="cuda", dtype=torch.int32)
+    ms = timeit(lambda: A.lower_bound(k, q))
+    emit(bench="lower_bound", n=n, queries=q.numel(), ms=ms, Gqueries_per_s=q.numel() / ms / 1e6)
+    ms = timeit(lambda: torch.searchsorted(k, q))
+    emit(bench="lower_bound", impl="torch.searchsorted", n=n, queries=q.numel(), ms=ms,
+         Gqueries_per_s=q.numel() / ms / 1e6)
+    ms = timeit(lambda: A.max_element(x))
+    emit(bench="max_element", n=n, ms=ms, GBps=4 * n / ms / 1e6)
+    ms = timeit(lambda: torch.argmax(x).item())
+    emit(bench="max_element", impl="torch.argmax", n=n, ms=ms, GBps=4 * n / ms / 1e6)
+    keys = torch.randint(0, 256, (n,), device="cuda", dtype=torch.int32)
+    ms = timeit(lambda: A.counting_sort(keys, 256))
+    emit(bench="counting_sort", n=n, num_keys=256, ms=ms, Gkeys_per_s=n / ms / 1e6)
 
 
 def bench_misc(emit, timeit):

@@ -100,3 +100,7 @@ CME_EXPORT int cme_workqueue_segment_sums(const int* offsets, int nseg, const fl
     hipLaunchKernelGGL(workqueue_kernel, dim3(4 * kNumCU), dim3(256), 0, s, offsets, nseg, v, out, head);
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(monte_carlo_pi, 256, mc_pi_kernel);
+CME_REGISTER_KERNEL(global_max, 256, global_max_kernel);

@@ -314,3 +314,6 @@ CME_EXPORT int cme_heat_dist_run(void* comm, void* buf0, void* buf1, int pitch, 
                             ext, tblock, rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
                             exchange_first, cur_out, as_stream(stream));
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(halo_pack_f32, 256, pack_block_kernel<float>);

@@ -200,3 +200,7 @@ CME_EXPORT int cme_copy_tune(const void* in, void* out, long long nbytes, int mo
 #undef CT
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(shift_cipher_u128, 256, shift_u128_kernel<4>);
+CME_REGISTER_KERNEL(copy_chunk, 256, copy_chunk_kernel<4>);

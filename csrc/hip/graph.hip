@@ -123,3 +123,7 @@ CME_EXPORT int cme_pr_propagate(const uint32_t* idx, const uint32_t* edges, cons
     }
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(pagerank_ref, 256, pr_ref_kernel);
+CME_REGISTER_KERNEL(pagerank_group8, 256, pr_group_kernel<8>);

@@ -513,3 +513,10 @@ CME_EXPORT int cme_heat_stream_tune_f32(const float* prev, float* curr, int pitc
         default: return (int)hipErrorInvalidValue;
     }
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(heat_naive_f32_o8, 256, heat_naive_kernel<float, 8>);
+CME_REGISTER_KERNEL(heat_lds_f32_o8, 256, heat_lds_kernel<float, 8, 32, 1>);
+CME_REGISTER_KERNEL(heat_stream_f32_o8, 256, heat_stream_kernel<float, 8, 4>);
+CME_REGISTER_KERNEL(heat_stream2_f32_o8, 256, heat_stream2_kernel<float, 8, 4>);
+CME_REGISTER_KERNEL(heat_stream2_f64_o8, 256, heat_stream2_kernel<double, 8, 2>);

@@ -751,3 +751,9 @@ CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flag
                            tiles, timeout, (uint32_t)(it + 1));
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kScanItemsPerLane / 4>);
+CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
+CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
+CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true>);

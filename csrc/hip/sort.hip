@@ -329,3 +329,9 @@ CME_EXPORT int cme_merge_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
     }
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel);
+CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
+CME_REGISTER_KERNEL(bitonic_tile, 256, bitonic_tile_kernel<false>);
+CME_REGISTER_KERNEL(merge_pass, 256, merge_pass_kernel<false>);

@@ -162,3 +162,10 @@ CME_EXPORT int cme_spmv_coo(int nrows, long long nnz, const int* row, const int*
     }
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(spmv_csr_scalar, 256, csr_scalar_kernel);
+CME_REGISTER_KERNEL(spmv_csr_vector8, 256, csr_vector_kernel<8>);
+CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);
+CME_REGISTER_KERNEL(spmv_dia, 256, dia_kernel);
+CME_REGISTER_KERNEL(spmv_coo, 256, coo_kernel);

@@ -236,3 +236,8 @@ CME_EXPORT int cme_vigenere(const uint8_t* in, long long n, const int* shifts, i
                        period, sign, out);
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(histogram_u8, 256, histogram_u8_kernel);
+CME_REGISTER_KERNEL(match_count, 256, match_count_kernel);
+CME_REGISTER_KERNEL(vigenere, 256, vigenere_kernel);

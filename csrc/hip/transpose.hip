@@ -130,3 +130,8 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
     }
     CME_LAUNCH_STATUS();
 }
+
+// kernels in the occupancy / resource report (cme_kernel_query)
+CME_REGISTER_KERNEL(transpose_naive, 256, naive_kernel);
+CME_REGISTER_KERNEL(transpose_lds_pad, 256, tile_kernel<1, 0>);
+CME_REGISTER_KERNEL(transpose_vec, 256, vec_kernel);

@@ -12,6 +12,15 @@
 
 #define CME_EXPORT extern "C" __attribute__((visibility("default")))
 
+// Kernel registry (for the occupancy / resource report, cme_kernel_query):
+// every translation unit registers its main kernels with the block size it
+// launches them with. Defined in runtime.hip.
+namespace cme {
+void register_kernel(const char* name, const void* fn, int block);
+}
+#define CME_REGISTER_KERNEL(tag, block, ...) \
+    static const int cme_reg_##tag = (::cme::register_kernel(#tag, reinterpret_cast<const void*>(&__VA_ARGS__), block), 0)
+
 // Wave64 is the CDNA execution quantum; never assume 32.
 constexpr int kWave = 64;
 // MI355X: 256 CUs in 8 XCDs.

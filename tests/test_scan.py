@@ -150,10 +150,11 @@ def test_segscan_gpu(gpu, nseg, bitmask):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(37035, 3128, 6), (3_105_536, 1_000_004, 3), (4_000_000, 1999, 3)])
-def test_spmv_scan_gpu_vs_fp64(gpu, shape):
+@pytest.mark.parametrize("algo", ["lookback", "wave", "serial"])
+def test_spmv_scan_gpu_vs_fp64(gpu, shape, algo):
     n, p, N = shape
     prob = generate(n, p, 10000, N, seed=5)
-    sol = SpmvScanSolver(prob, gpu)
+    sol = SpmvScanSolver(prob, gpu, algo)
     b = sol.run().cpu().numpy()
     e = errors(reference_solution(prob), b)
     assert e["relL2"] < 1e-5, e

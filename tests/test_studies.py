@@ -1,0 +1,64 @@
+"""Lecture studies: divergence / coalescing kernels, summation accuracy,
+kernel occupancy report."""
+import numpy as np
+import pytest
+import torch
+
+from cme213x.ops import studies
+
+
+def test_summation_accuracy_ordering():
+    rows = studies.summation_study(sizes=(1 << 16, 1 << 22))
+    big = rows[-1]
+    # serial error grows ~n eps; pairwise / Kahan stay near eps
+    assert big["serial"] > 10 * big["pairwise"]
+    assert big["kahan"] <= big["pairwise"] * 1.01 + 1e-9
+    assert big["kahan"] < 1e-6
+
+
+def test_littles_law():
+    from cme213x.utils.occupancy import littles_law
+
+    ll = littles_law(8e12, 1e-6, 256)
+    assert ll["bytes_in_flight"] == pytest.approx(8e6)
+    assert ll["bytes_per_cu"] == pytest.approx(8e6 / 256)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1, 7, 64, 128])
+def test_divergence_kernel(gpu, stride):
+    n = 100_000
+    out = torch.empty(n, device=gpu)
+    studies.divergence(out, stride, 64)
+    ref = studies.divergence_reference(n, stride, 64)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,offset", [(1, 0), (1, 3), (4, 1), (33, 7)])
+def test_strided_copy(gpu, stride, offset):
+    n = 50_000
+    src = torch.rand(n * stride + offset + 1, device=gpu)
+    out = studies.strided_copy(src, n, stride, offset)
+    assert torch.equal(out, src[offset:offset + (n - 1) * stride + 1:stride])
+
+
+@pytest.mark.gpu
+def test_gpu_tree_reduction_beats_serial(gpu):
+    rows = studies.summation_study(sizes=(1 << 22,), device=gpu)
+    r = rows[0]
+    assert r["gpu_tree"] < r["serial"] and r["gpu_vector"] < r["serial"]
+
+
+@pytest.mark.gpu
+def test_occupancy_report(gpu):
+    from cme213x.utils.occupancy import format_report, kernel_report
+
+    rows = kernel_report()
+    names = {r["kernel"] for r in rows}
+    assert {"heat_stream2_f32_o8", "sgemm_mfma", "scan_rts_scan_f32", "segscan_wave"} <= names
+    for r in rows:
+        assert r["blocks_per_cu"] >= 1, r
+        assert 0 < r["vgprs"] <= 512, r
+        assert r["scratch_bytes"] == 0, f"{r['kernel']} spills to scratch"
+    assert "heat_stream2_f32_o8" in format_report(rows)
