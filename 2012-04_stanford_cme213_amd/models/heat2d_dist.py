@@ -113,7 +113,7 @@ class DistHeat:
 
     def __init__(self, params: SimParams, comm: Comm | None = None, dtype=torch.float32, device="cpu",
                  local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream",
-                 tblock: int = 1):
+                 tblock: int = 1, fma: bool = False):
         self.p = params
         self.comm = comm or LoopbackComm()
         self.world = world or self.comm.size
@@ -122,7 +122,8 @@ class DistHeat:
             raise ValueError("multi-process runs own exactly one subdomain per rank")
         if tblock not in (1, 2):
             raise ValueError("tblock must be 1 or 2")
-        self.variant = variant
+        self.fma = bool(fma)
+        self.variant = "fma" if self.fma else variant
         self.tblock = tblock
         self.device = torch.device(device)
         self.subs: dict[int, _Sub] = {}
@@ -234,7 +235,7 @@ class DistHeat:
                 g = s.grid
                 ext = _ext_region(s)
                 for reg in regions_of(s, 2 * g.B):
-                    heat_step2(g.buf[k], g.buf[1 - k], reg, ext, g.order, g.xcfl, g.ycfl)
+                    heat_step2(g.buf[k], g.buf[1 - k], reg, ext, g.order, g.xcfl, g.ycfl, fma=self.fma)
 
         if sync:
             sweep(_interior_regions)
@@ -311,7 +312,7 @@ class DistHeat:
         cur_out = ctypes.c_int(0)
         _ext.call_hip("cme_heat_dist_run", rccl.handle, g.buf[0].data_ptr(), g.buf[1].data_ptr(), g.pitch, g.gy,
                       plan["interior"].data_ptr(), plan["interior"].shape[0], plan["border"].data_ptr(),
-                      plan["border"].shape[0], plan["ext"].data_ptr(), self.tblock,
+                      plan["border"].shape[0], plan["ext"].data_ptr(), self.tblock, int(self.fma),
                       plan["rows"].data_ptr(), plan["rows"].shape[0],
                       plan["cols"].data_ptr(), plan["cols"].shape[0], plan["stage"].data_ptr(),
                       0 if g.dtype == torch.float32 else 1, g.order, g.xcfl, g.ycfl, iters, g.cur, int(sync), 0,

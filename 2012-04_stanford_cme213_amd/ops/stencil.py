@@ -18,17 +18,23 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiipp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiippiffip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiippiddip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipipipipiiddiiiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiippiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiippiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipiipipipiiddiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f64", "ppiiiiiiddi")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f32", "ppiiiiiiff")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f64", "ppiiiiiidd")
 
-VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4}
+VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
+            "stream2_fma": 5, "stream_fma": 6, "fma": 6}
 # variants that advance more than one timestep per launch (multi-step drivers only)
-MULTISTEP = {"stream2"}
+MULTISTEP = {"stream2", "stream2_fma"}
+# FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
+# std::fma oracle, every other variant name the exact (contraction-off) one
+FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -58,12 +64,14 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
         _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, xb, xe, yb, ye, order,
                       VARIANTS[variant], xcfl, ycfl, chunk, _ext.stream_ptr(prev.device))
     else:
-        name = "cme_cpu_heat_step_f64" if f64 else "cme_cpu_heat_step_f32"
+        fma = "_fma" if variant in FMA_VARIANTS else ""
+        name = f"cme_cpu_heat_step{fma}_f64" if f64 else f"cme_cpu_heat_step{fma}_f32"
         _ext.call_cpu(name, prev.data_ptr(), curr.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl)
 
 
 def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, int, int],
-               ext: tuple[int, int, int, int], order: int, xcfl: float, ycfl: float, chunk: int = 0) -> None:
+               ext: tuple[int, int, int, int], order: int, xcfl: float, ycfl: float, chunk: int = 0,
+               fma: bool = False) -> None:
     """TWO timesteps in one HBM pass (GPU only): the intermediate step covers
     ``ext`` (``region`` grown by at most B cells, e.g. into a 2B-deep halo),
     the second writes ``curr[region]``. Cells of ``ext`` outside the grid's
@@ -71,16 +79,17 @@ def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, i
     (ext, then region). On CPU it runs exactly that (through a temporary)."""
     _check(prev, curr)
     if not prev.is_cuda:
+        v = "fma" if fma else "naive"
         tmp = prev.clone()
-        heat_step(prev, tmp, ext, order, xcfl, ycfl)
-        heat_step(tmp, curr, region, order, xcfl, ycfl)
+        heat_step(prev, tmp, ext, order, xcfl, ycfl, v)
+        heat_step(tmp, curr, region, order, xcfl, ycfl, v)
         return
     rows, pitch = prev.shape
     r = (ctypes.c_int * 4)(*map(int, region))
     e = (ctypes.c_int * 4)(*map(int, ext))
     name = "cme_heat_step2_f64" if prev.dtype == torch.float64 else "cme_heat_step2_f32"
     _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), ctypes.addressof(e),
-                  order, xcfl, ycfl, chunk, _ext.stream_ptr(prev.device))
+                  order, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
 
 
 def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
@@ -99,6 +108,10 @@ def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int]
         _ext.call_hip(name, a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, VARIANTS[variant],
                       xcfl, ycfl, iters, chunk, ctypes.addressof(final), _ext.stream_ptr(a.device))
         return b if final.value else a
+    elif variant in FMA_VARIANTS:
+        for i in range(iters):
+            src, dst = (a, b) if i % 2 == 0 else (b, a)
+            heat_step(src, dst, region, order, xcfl, ycfl, "fma")
     else:
         name = "cme_cpu_heat_run_f64" if f64 else "cme_cpu_heat_run_f32"
         _ext.call_cpu(name, a.data_ptr(), b.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl, iters)

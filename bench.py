@@ -46,8 +46,8 @@ def native_selftest(comm, rccl, dev, args) -> bool:
 
     p = SimParams(nx=1024, ny=1024, iters=6, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
-    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock)
-    b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1)
+    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma))
+    b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1, fma=bool(args.fma))
     # non-uniform interior so a stale or misplaced halo changes the answer
     for sim in (a, b):
         s = next(iter(sim.subs.values()))
@@ -79,6 +79,9 @@ def main() -> int:
     ap.add_argument("--method", type=int, default=1, help="1 = 1-D stripes, 2 = 2-D blocks")
     ap.add_argument("--mode", choices=["async", "sync"], default="async")
     ap.add_argument("--variant", default="stream")
+    ap.add_argument("--fma", type=int, choices=[0, 1], default=1,
+                    help="FMA-contracted stencil (what nvcc emits for the reference's GPU kernels); 0 = exact "
+                         "contraction-off arithmetic, bitwise equal to the non-FMA CPU oracle")
     ap.add_argument("--tblock", type=int, choices=[1, 2], default=2,
                     help="timesteps per halo exchange / per HBM pass (2 = temporal blocking, 2B-deep halos)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
@@ -117,7 +120,7 @@ def main() -> int:
             native_ok = native_selftest(comm, rccl, dev, args)
     use_native = rccl is not None and native_ok
 
-    sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock)
+    sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma))
 
     def run(k):
         if use_native:
@@ -173,7 +176,9 @@ def main() -> int:
                 "global_batch": pts,
                 "seq_len": 1,
                 "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
-                "variant": args.variant if args.tblock == 1 else "stream2 (2 steps/pass)",
+                "variant": (args.variant if args.tblock == 1 else "stream2 (2 steps/pass)")
+                + (" fma" if args.fma else " exact"),
+                "fma": bool(args.fma),
                 "tblock": args.tblock,
                 "loop": "native-rccl" if use_native else ("torch.distributed" if comm.size > 1 else "single"),
             },

@@ -13,7 +13,7 @@ using namespace cme;
 
 namespace {
 
-template <typename T, int ORDER>
+template <typename T, int ORDER, bool FMA>
 void heat_region(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int ye, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
 #pragma omp parallel for schedule(static)
@@ -28,17 +28,17 @@ void heat_region(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int 
                 ym[k] = row[x - (ptrdiff_t)(k + 1) * pitch];
                 yp[k] = row[x + (ptrdiff_t)(k + 1) * pitch];
             }
-            out[x] = heat_update<ORDER>(row[x], xm, xp, ym, yp, xcfl, ycfl);
+            out[x] = heat_update_sel<ORDER, FMA>(row[x], xm, xp, ym, yp, xcfl, ycfl);
         }
     }
 }
 
-template <typename T>
+template <typename T, bool FMA = false>
 int heat_dispatch(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int ye, int order, T xcfl, T ycfl) {
     switch (order) {
-        case 2: heat_region<T, 2>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
-        case 4: heat_region<T, 4>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
-        case 8: heat_region<T, 8>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
+        case 2: heat_region<T, 2, FMA>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
+        case 4: heat_region<T, 4, FMA>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
+        case 8: heat_region<T, 8, FMA>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
         default: return 1;
     }
 }
@@ -71,4 +71,16 @@ CME_CPU_EXPORT int cme_cpu_heat_run_f64(double* a, double* b, int pitch, int xb,
         if (rc) return rc;
     }
     return 0;
+}
+
+// FMA-contracted oracle (heat_update_fma): bitwise reference for the GPU's
+// FMA stencil variants (std::fma is correctly rounded).
+CME_CPU_EXPORT int cme_cpu_heat_step_fma_f32(const float* prev, float* curr, int pitch, int xb, int xe, int yb, int ye,
+                                             int order, float xcfl, float ycfl) {
+    return heat_dispatch<float, true>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
+}
+
+CME_CPU_EXPORT int cme_cpu_heat_step_fma_f64(const double* prev, double* curr, int pitch, int xb, int xe, int yb,
+                                             int ye, int order, double xcfl, double ycfl) {
+    return heat_dispatch<double, true>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
 }

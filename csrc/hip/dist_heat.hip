@@ -22,9 +22,9 @@ extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int 
 extern "C" int cme_heat_step_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, double xcfl, double ycfl, int chunk, void* stream);
 extern "C" int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, float xcfl, float ycfl, int chunk, void* stream);
+                                  int order, float xcfl, float ycfl, int chunk, int fma, void* stream);
 extern "C" int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, double xcfl, double ycfl, int chunk, void* stream);
+                                  int order, double xcfl, double ycfl, int chunk, int fma, void* stream);
 
 #define CME_TRY_INT(expr)                 \
     do {                                  \
@@ -156,33 +156,35 @@ int get_ctx(DistCtx** out) {
     return 0;
 }
 
+// single step: streaming kernel, exact (variant 2) or FMA (variant 6)
 template <typename T>
-int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T xcfl, T ycfl, hipStream_t s);
+int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T xcfl, T ycfl, int fma,
+                hipStream_t s);
 
 template <>
 int step_region<float>(const float* p, float* c, int pitch, int gy, const int* r, int order, float xcfl, float ycfl,
-                       hipStream_t s) {
-    return cme_heat_step_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, 2, xcfl, ycfl, 0, (void*)s);
+                       int fma, hipStream_t s) {
+    return cme_heat_step_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
 }
 template <>
 int step_region<double>(const double* p, double* c, int pitch, int gy, const int* r, int order, double xcfl,
-                        double ycfl, hipStream_t s) {
-    return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, 2, xcfl, ycfl, 0, (void*)s);
+                        double ycfl, int fma, hipStream_t s) {
+    return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
 }
 
 template <typename T>
 int step2_region(const T* p, T* c, int pitch, int gy, const int* r, const int* ext, int order, T xcfl, T ycfl,
-                 hipStream_t s);
+                 int fma, hipStream_t s);
 
 template <>
 int step2_region<float>(const float* p, float* c, int pitch, int gy, const int* r, const int* ext, int order,
-                        float xcfl, float ycfl, hipStream_t s) {
-    return cme_heat_step2_f32(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, (void*)s);
+                        float xcfl, float ycfl, int fma, hipStream_t s) {
+    return cme_heat_step2_f32(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, fma, (void*)s);
 }
 template <>
 int step2_region<double>(const double* p, double* c, int pitch, int gy, const int* r, const int* ext, int order,
-                         double xcfl, double ycfl, hipStream_t s) {
-    return cme_heat_step2_f64(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, (void*)s);
+                         double xcfl, double ycfl, int fma, hipStream_t s) {
+    return cme_heat_step2_f64(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, fma, (void*)s);
 }
 
 // Exchange plan for buffer `g`:
@@ -237,7 +239,7 @@ int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n
 
 template <typename T>
 int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* interior, int n_int, const int* border,
-             int n_b, const int* ext, int tblock, const long long* rows, int n_rows, const int* cols, int n_cols, T* stage, int order, T xcfl,
+             int n_b, const int* ext, int tblock, int fma, const long long* rows, int n_rows, const int* cols, int n_cols, T* stage, int order, T xcfl,
              T ycfl, int iters, int cur, int sync, int exchange_first, int* cur_out, hipStream_t s) {
     DistCtx* ctx;
     CME_TRY_INT(get_ctx(&ctx));
@@ -261,8 +263,8 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
         const bool two = tblock == 2 && it + 1 < iters;
         auto sweep = [&](const int* regs, int n) -> int {
             for (int i = 0; i < n; ++i) {
-                int rc = two ? step2_region<T>(p, c, pitch, gy, regs + 4 * i, ext, order, xcfl, ycfl, s)
-                             : step_region<T>(p, c, pitch, gy, regs + 4 * i, order, xcfl, ycfl, s);
+                int rc = two ? step2_region<T>(p, c, pitch, gy, regs + 4 * i, ext, order, xcfl, ycfl, fma, s)
+                             : step_region<T>(p, c, pitch, gy, regs + 4 * i, order, xcfl, ycfl, fma, s);
                 if (rc) return rc;
             }
             return 0;
@@ -301,17 +303,18 @@ int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* in
 // The distributed heat loop (see dist_run). dtype 0 = f32, 1 = f64.
 // tblock 1: one step per exchange; 2: two steps per exchange (needs 2B-deep
 // halos, `interior` shrunk by 2B on neighbour sides, `ext` = owned region
-// grown by B on neighbour sides).
+// grown by B on neighbour sides). fma: FMA-contracted stencil.
 CME_EXPORT int cme_heat_dist_run(void* comm, void* buf0, void* buf1, int pitch, int gy, const int* interior, int n_int,
-                                 const int* border, int n_b, const int* ext, int tblock, const long long* rows, int n_rows, const int* cols,
+                                 const int* border, int n_b, const int* ext, int tblock, int fma,
+                                 const long long* rows, int n_rows, const int* cols,
                                  int n_cols, void* stage, int dtype, int order, double xcfl, double ycfl, int iters,
                                  int cur, int sync, int exchange_first, int* cur_out, void* stream) {
     if (dtype == 0)
         return dist_run<float>((ncclComm_t)comm, (float*)buf0, (float*)buf1, pitch, gy, interior, n_int, border, n_b,
-                               ext, tblock, rows, n_rows, cols, n_cols, (float*)stage, order, (float)xcfl, (float)ycfl, iters, cur,
+                               ext, tblock, fma, rows, n_rows, cols, n_cols, (float*)stage, order, (float)xcfl, (float)ycfl, iters, cur,
                                sync, exchange_first, cur_out, as_stream(stream));
     return dist_run<double>((ncclComm_t)comm, (double*)buf0, (double*)buf1, pitch, gy, interior, n_int, border, n_b,
-                            ext, tblock, rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
+                            ext, tblock, fma, rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
                             exchange_first, cur_out, as_stream(stream));
 }
 

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void heat_lds_kernel(const T* __restrict__ pre
 // ---------------------------------------------------------------- stream
 constexpr int kStripOut = 62 * 4;  // output columns per wave strip
 
-template <typename T, int ORDER, int RB, int WPB = 4, bool NT = false>
+template <typename T, int ORDER, int RB, int WPB = 4, bool NT = false, bool FMA = false>
 __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
                                                           int gy, int xb, int xe, int yb, int ye, int strips, int chunk,
                                                           int total_waves, T xcfl, T ycfl) {
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restri
                     ym[k] = win[r + B - (k + 1)][j];
                     yp[k] = win[r + B + (k + 1)][j];
                 }
-                o[j] = heat_update<ORDER>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+                o[j] = heat_update_sel<ORDER, FMA>(c[j], xm, xp, ym, yp, xcfl, ycfl);
             }
             const int yy = y + r;
             if (out_lane && yy < y1) {
@@ -186,18 +186,164 @@ __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restri
 // Temporal blocking: TWO timesteps per pass over HBM. The wave keeps an input
 // row window AND a window of step-1 rows in VGPRs; step-1 rows are produced
 // on lanes 1..62 (x-neighbours through DPP), step-2 rows on lanes 2..61
-// (4 x 60 = 240 output columns per strip). Cells outside the region keep
-// their input value in the intermediate state (fixed boundary cells), so the
-// result is bitwise identical to two single steps.
+// (4 x 60 = 240 output columns per strip). Cells outside the step-1 region
+// keep their input value in the intermediate state (fixed boundary cells), so
+// the result is bitwise identical to two single steps.
+//
+// Instruction diet (the kernel is VALU-bound once two steps share a pass):
+//  * both windows are rings indexed by compile-time slots; the main loop is
+//    unrolled over P = NW / gcd(NW, RB) phases, so advancing the window costs
+//    no register moves;
+//  * waves whose step-1 cells all lie inside the region skip the per-cell
+//    region select (wave-uniform branch into a CHECK=false instance); the
+//    step-2 value needs no select at all since only in-region cells are
+//    stored;
+//  * FMA=true evaluates the FMA-contracted stencil (heat_update_fma).
 constexpr int kStrip2Out = 60 * 4;
 
-template <typename T, int ORDER, int RB>
-__global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+template <typename T, int ORDER, int RB, bool FMA, bool CHECK>
+struct Stream2 {
+    static constexpr int B = HeatOrder<ORDER>::B;
+    static constexpr int NW = RB + 2 * B;           // rows per window
+    static constexpr int P = NW / cgcd(NW, RB);     // phases until the ring realigns
+
+    V4<T> in[NW];   // input rows; logical j = row r0 - B + j
+    V4<T> s1[NW];   // step-1 rows; logical j = row r0 - 2B + j
+    V4<T> nxt[RB];  // prefetched input rows
+    const T* src;
+    T* dst;
+    int pitch, gy, xbase;
+    bool out_lane, full_vec;
+    int y0, y1, xb, xe, xb1, xe1, yb1, ye1;
+    T xcfl, ycfl;
+    int r0;
+
+    __device__ __forceinline__ const T* row_ptr(int r) const {
+        r = r < 0 ? 0 : (r >= gy ? gy - 1 : r);
+        return src + (size_t)r * pitch;
+    }
+
+    // FTCS update of this lane's 4 columns for the row centred on ring slot
+    // (s_lo + B) % NW of window w.
+    template <bool MASK>
+    __device__ __forceinline__ V4<T> upd(const V4<T> (&w)[NW], int s_lo, int row) const {
+        const V4<T> c = w[(s_lo + B) % NW];
+        const V4<T> L = wave_shr1(c);
+        const V4<T> R = wave_shl1(c);
+        T rowv[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            rowv[j] = L[j];
+            rowv[4 + j] = c[j];
+            rowv[8 + j] = R[j];
+        }
+        bool row_in = true;
+        if constexpr (MASK) row_in = row >= yb1 && row < ye1;
+        V4<T> o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                xm[k] = rowv[4 + j - (k + 1)];
+                xp[k] = rowv[4 + j + (k + 1)];
+                ym[k] = w[(s_lo + B - (k + 1)) % NW][j];
+                yp[k] = w[(s_lo + B + (k + 1)) % NW][j];
+            }
+            const T u = heat_update_sel<ORDER, FMA>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+            if constexpr (MASK) {
+                const int x = xbase + j;
+                o[j] = (row_in && x >= xb1 && x < xe1) ? u : c[j];
+            } else {
+                o[j] = u;
+            }
+        }
+        return o;
+    }
+
+    template <int PH>
+    __device__ __forceinline__ bool phase() {
+        if (r0 - B >= y1) return false;
+        constexpr int S = (PH * RB) % NW;  // ring slot of logical row 0
+#pragma unroll
+        for (int i = 0; i < RB; ++i) in[(S + 2 * B + i) % NW] = nxt[i];
+        if (r0 + RB - B < y1) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) s1[(S + 2 * B + i) % NW] = upd<CHECK>(in, (S + i) % NW, r0 + i);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            const int y = r0 - B + i;
+            const V4<T> o = upd<false>(s1, (S + i) % NW, y);
+            if (y >= y0 && y < y1) {  // wave-uniform
+                T* d = dst + (size_t)y * pitch;
+                if constexpr (!CHECK) {
+                    // interior strip: every output lane holds 4 in-region cells
+                    if (out_lane) store4(d, o);
+                } else if (out_lane) {
+                    if (full_vec) {
+                        store4(d, o);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xbase + j >= xb && xbase + j < xe) d[j] = o[j];
+                    }
+                }
+            }
+        }
+        r0 += RB;
+        if constexpr (PH + 1 < P)
+            return phase<PH + 1>();
+        else
+            return true;
+    }
+
+    __device__ __forceinline__ void run() {
+        r0 = y0 - B;
+#pragma unroll
+        for (int i = 0; i < 2 * B; ++i) in[i] = load4(row_ptr(r0 - B + i));
+#pragma unroll
+        for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + B + i));
+        while (phase<0>()) {
+        }
+    }
+};
+
+template <typename T, int ORDER, int RB, bool FMA, bool CHECK>
+__device__ __forceinline__ void stream2_run(const T* src, T* dst, int pitch, int gy, int xbase, bool out_lane,
+                                            bool full_vec, int y0, int y1, int xb, int xe, int xb1, int xe1, int yb1,
+                                            int ye1, T xcfl, T ycfl) {
+    Stream2<T, ORDER, RB, FMA, CHECK> st;
+    st.src = src;
+    st.dst = dst;
+    st.pitch = pitch;
+    st.gy = gy;
+    st.xbase = xbase;
+    st.out_lane = out_lane;
+    st.full_vec = full_vec;
+    st.y0 = y0;
+    st.y1 = y1;
+    st.xb = xb;
+    st.xe = xe;
+    st.xb1 = xb1;
+    st.xe1 = xe1;
+    st.yb1 = yb1;
+    st.ye1 = ye1;
+    st.xcfl = xcfl;
+    st.ycfl = ycfl;
+    st.run();
+}
+
+template <typename T, int ORDER, int RB, bool FMA, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_stream2_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
                                                            int gy, int xb, int xe, int yb, int ye, int xb1,
                                                            int xe1, int yb1, int ye1, int strips, int chunk,
                                                            int total_waves, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
-    constexpr int NW = RB + 2 * B;
     const int lane = lane_id();
     const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
     if (wave >= total_waves) return;
@@ -210,82 +356,17 @@ __global__ __launch_bounds__(256) void heat_stream2_kernel(const T* __restrict__
     const int xl = min(max(xbase, 0), pitch - 4);
     const bool out_lane = (lane >= 2) && (lane <= 61) && (xbase < xe) && (xbase + 4 > xb);
     const bool full_vec = (xbase >= xb) && (xbase + 4 <= xe);
-    const T* src = prev + xl;
-    T* dst = curr + xl;
-    auto row_ptr = [&](int r) -> const T* {
-        r = r < 0 ? 0 : (r >= gy ? gy - 1 : r);
-        return src + (size_t)r * pitch;
-    };
-    // one FTCS update of the 4 columns of this lane for a row whose window is
-    // w[k0 .. k0+2B]; cells outside region [rxb,rxe)x[ryb,rye) keep their value
-    auto update = [&](const V4<T>* w, int k0, int row, int rxb, int rxe, int ryb, int rye) -> V4<T> {
-        const V4<T> c = w[k0 + B];
-        const V4<T> L = wave_shr1(c);
-        const V4<T> R = wave_shl1(c);
-        T rowv[12];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            rowv[j] = L[j];
-            rowv[4 + j] = c[j];
-            rowv[8 + j] = R[j];
-        }
-        V4<T> o;
-        const bool row_in = row >= ryb && row < rye;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            T xm[B], xp[B], ym[B], yp[B];
-#pragma unroll
-            for (int k = 0; k < B; ++k) {
-                xm[k] = rowv[4 + j - (k + 1)];
-                xp[k] = rowv[4 + j + (k + 1)];
-                ym[k] = w[k0 + B - (k + 1)][j];
-                yp[k] = w[k0 + B + (k + 1)][j];
-            }
-            const T u = heat_update<ORDER>(c[j], xm, xp, ym, yp, xcfl, ycfl);
-            const int x = xbase + j;
-            o[j] = (row_in && x >= rxb && x < rxe) ? u : c[j];
-        }
-        return o;
-    };
-
-    V4<T> in[NW];   // input rows r0-B .. r0+RB-1+B
-    V4<T> s1[NW];   // step-1 rows r0-2B .. r0+RB-1
-    V4<T> nxt[RB];
-    int r0 = y0 - B;  // first step-1 row of the current block
-#pragma unroll
-    for (int i = 0; i < 2 * B; ++i) in[i] = load4(row_ptr(r0 - B + i));
-#pragma unroll
-    for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + B + i));
-    for (; r0 - B < y1; r0 += RB) {
-#pragma unroll
-        for (int i = 0; i < RB; ++i) in[2 * B + i] = nxt[i];
-        if (r0 + RB - B < y1) {
-#pragma unroll
-            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
-        }
-#pragma unroll
-        for (int i = 0; i < RB; ++i) s1[2 * B + i] = update(in, i, r0 + i, xb1, xe1, yb1, ye1);
-#pragma unroll
-        for (int i = 0; i < RB; ++i) {
-            const int y = r0 - B + i;
-            const V4<T> o = update(s1, i, y, xb, xe, yb, ye);
-            if (out_lane && y >= y0 && y < y1) {
-                T* d = dst + (size_t)y * pitch;
-                if (full_vec) {
-                    store4(d, o);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (xbase + j >= xb && xbase + j < xe) d[j] = o[j];
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 2 * B; ++i) {
-            in[i] = in[RB + i];
-            s1[i] = s1[RB + i];
-        }
-    }
+    // step-1 cells that matter: columns xs-4 .. xs+243 (lanes 1..62), rows
+    // y0-B .. y1+B-1; all inside the step-1 region -> no per-cell select; and
+    // output columns xs .. xs+239 all inside [xb, xe) -> plain vector stores
+    const bool inside = (xs - 4 >= xb1) && (xs + 244 <= xe1) && (y0 - B >= yb1) && (y1 + B <= ye1) &&
+                        (xs >= xb) && (xs + kStrip2Out <= xe);
+    if (inside)
+        stream2_run<T, ORDER, RB, FMA, false>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1, xb,
+                                              xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+    else
+        stream2_run<T, ORDER, RB, FMA, true>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1, xb,
+                                             xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -296,26 +377,29 @@ struct Region {
 // Two-step pass: output region `g`; step-1 (intermediate) region `g1` must
 // contain g and may extend at most B cells beyond it (into a 2B-deep halo,
 // for the distributed loop); cells outside g1 keep their input value.
-template <typename T, int ORDER>
+// Defaults from benchmarks/tune_heat2.py (16384^2, order 8; profiles/
+// heat_stream2_tune.md): rows per block RB and a target wave count that sets
+// the row chunk (more, shorter chunks win for the lighter FMA kernel).
+template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
 int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
                    hipStream_t s) {
-    constexpr int RB = sizeof(T) == 4 ? 4 : 2;
     const int H = g.ye - g.yb;
     if (H <= 0 || g.xe <= g.xb) return 0;
     const int x_lo = g.xb & ~3;
     const int strips = (int)cdiv(g.xe - x_lo, kStrip2Out);
     int chunk = chunk_hint;
     if (chunk <= 0) {
-        const long target_waves = 256L * 12;
+        const long target_waves = 256L * (sizeof(T) == 4 ? (FMA ? 128 : 48) : 24);
         long rows = ((long)strips * H + target_waves - 1) / target_waves;
-        rows = rows < 4 * RB ? 4 * RB : rows;
+        const long lo = 4 * RB > 16 ? 4 * RB : 16;
+        rows = rows < lo ? lo : rows;
         rows = rows > 512 ? 512 : rows;
         chunk = (int)rows;
     }
     chunk = ((chunk + RB - 1) / RB) * RB;
     const int chunks = (int)cdiv(H, chunk);
     const int total_waves = strips * chunks;
-    hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
+    hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB, FMA, WPE>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
                        pitch, gy, g.xb, g.xe, g.yb, g.ye, g1.xb, g1.xe, g1.yb, g1.ye, strips, chunk, total_waves, xcfl,
                        ycfl);
     CME_LAUNCH_STATUS();
@@ -339,9 +423,10 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         dim3 grid(cdiv(W, 64), cdiv(H, TY));
         hipLaunchKernelGGL((heat_lds_kernel<T, ORDER, TY, 1>), grid, dim3(256), 0, s, prev, curr, pitch, gy, g.xb,
                            g.xe, g.yb, g.ye, xcfl, ycfl);
-    } else if (variant == 4) {
+    } else if (variant == 4 || variant == 5) {
         // TWO timesteps per launch (temporal blocking), step-1 region = output
-        return launch_stream2<T, ORDER>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s);
+        return variant == 4 ? launch_stream2<T, ORDER, false>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s)
+                            : launch_stream2<T, ORDER, true>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s);
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -364,8 +449,13 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         chunk = ((chunk + RB - 1) / RB) * RB;
         const int chunks = (int)cdiv(H, chunk);
         const int total_waves = strips * chunks;
-        hipLaunchKernelGGL((heat_stream_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
-                           pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
+        if (variant == 6)
+            hipLaunchKernelGGL((heat_stream_kernel<T, ORDER, RB, 4, false, true>), dim3(cdiv(total_waves, 4)),
+                               dim3(256), 0, s, prev, curr, pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk,
+                               total_waves, xcfl, ycfl);
+        else
+            hipLaunchKernelGGL((heat_stream_kernel<T, ORDER, RB>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev,
+                               curr, pitch, gy, g.xb, g.xe, g.yb, g.ye, strips, chunk, total_waves, xcfl, ycfl);
     }
     CME_LAUNCH_STATUS();
 }
@@ -381,34 +471,44 @@ int dispatch_heat(int order, int variant, const T* prev, T* curr, int pitch, int
     }
 }
 
-template <typename T>
-int dispatch_stream2(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
-                     int chunk, hipStream_t s) {
+template <typename T, bool FMA>
+int dispatch_stream2_t(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
+                       int chunk, hipStream_t s) {
     switch (order) {
-        case 2: return launch_stream2<T, 2>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
-        case 4: return launch_stream2<T, 4>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
-        case 8: return launch_stream2<T, 8>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 2: return launch_stream2<T, 2, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 4: return launch_stream2<T, 4, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 8: return launch_stream2<T, 8, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
         default: return (int)hipErrorInvalidValue;
     }
+}
+
+template <typename T>
+int dispatch_stream2(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
+                     int chunk, int fma, hipStream_t s) {
+    return fma ? dispatch_stream2_t<T, true>(order, prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s)
+               : dispatch_stream2_t<T, false>(order, prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
 }
 
 }  // namespace
 
 // TWO timesteps in one pass: curr[out] = FTCS^2(prev) where the intermediate
 // step is applied on region `ext` (out grown by <= B cells into a halo).
+// fma: 0 exact (contraction off), 1 FMA-contracted stencil.
 CME_EXPORT int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, float xcfl, float ycfl, int chunk, void* stream) {
+                                  int order, float xcfl, float ycfl, int chunk, int fma, void* stream) {
     return dispatch_stream2<float>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
-                                   Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, as_stream(stream));
+                                   Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, fma, as_stream(stream));
 }
 
 CME_EXPORT int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, double xcfl, double ycfl, int chunk, void* stream) {
+                                  int order, double xcfl, double ycfl, int chunk, int fma, void* stream) {
     return dispatch_stream2<double>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
-                                    Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, as_stream(stream));
+                                    Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, fma,
+                                    as_stream(stream));
 }
 
-// variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO steps)
+// variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO
+// steps), 5 stream2 FMA (TWO steps), 6 stream FMA
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -424,7 +524,8 @@ CME_EXPORT int cme_heat_step_f64(const double* prev, double* curr, int pitch, in
 // Multi-step driver: `iters` sweeps of the full region in one call (buffers
 // a/b, first sweep reads a). Avoids per-iteration host round trips (the
 // reference synchronises after every launch: 2dHeat_solution.cu:549).
-// variant 4 advances TWO steps per launch (+ one single step for odd iters).
+// variants 4/5 advance TWO steps per launch (+ one single step, variant 2/6,
+// for odd iters).
 // *final_idx = 0 if the result is in a, 1 if in b.
 template <typename T>
 int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int variant, T xcfl, T ycfl, int iters,
@@ -432,13 +533,13 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int cur = 0;
     T* bufs[2] = {a, b};
     int i = 0;
-    if (variant == 4) {
+    if (variant == 4 || variant == 5) {
         for (; i + 1 < iters; i += 2) {
-            int rc = dispatch_heat<T>(order, 4, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
+            int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
             if (rc) return rc;
             cur ^= 1;
         }
-        variant = 2;
+        variant = variant == 4 ? 2 : 6;
     }
     for (; i < iters; ++i) {
         int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
@@ -514,9 +615,53 @@ CME_EXPORT int cme_heat_stream_tune_f32(const float* prev, float* curr, int pitc
     }
 }
 
+// Tuning entry for the two-step kernel (order 8): rows per block rb 2/4/8 and
+// a waves-per-EU register cap wpe 1 (none)/2/3/4, exact or FMA, f32 or f64.
+// Used by benchmarks/tune_heat.py --stream2; production uses the defaults.
+namespace {
+template <typename T, bool FMA, int RB>
+int tune2_wpe(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, int chunk, int wpe, hipStream_t s) {
+    switch (wpe) {
+        case 1: return launch_stream2<T, 8, FMA, RB, 1>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk, s);
+        case 2: return launch_stream2<T, 8, FMA, RB, 2>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk, s);
+        case 3: return launch_stream2<T, 8, FMA, RB, 3>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk, s);
+        case 4: return launch_stream2<T, 8, FMA, RB, 4>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+template <typename T, bool FMA>
+int tune2_rb(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, int chunk, int rb, int wpe,
+             hipStream_t s) {
+    switch (rb) {
+        case 2: return tune2_wpe<T, FMA, 2>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, wpe, s);
+        case 4: return tune2_wpe<T, FMA, 4>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, wpe, s);
+        case 8: return tune2_wpe<T, FMA, 8>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, wpe, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_stream2_tune(const void* prev, void* curr, int dtype, int pitch, int gy, int xb, int xe,
+                                     int yb, int ye, double xcfl, double ycfl, int chunk, int rb, int wpe, int fma,
+                                     void* stream) {
+    hipStream_t s = as_stream(stream);
+    const Region g{xb, xe, yb, ye};
+    if (dtype == 0) {
+        const float* p = (const float*)prev;
+        float* c = (float*)curr;
+        return fma ? tune2_rb<float, true>(p, c, pitch, gy, g, (float)xcfl, (float)ycfl, chunk, rb, wpe, s)
+                   : tune2_rb<float, false>(p, c, pitch, gy, g, (float)xcfl, (float)ycfl, chunk, rb, wpe, s);
+    }
+    const double* p = (const double*)prev;
+    double* c = (double*)curr;
+    return fma ? tune2_rb<double, true>(p, c, pitch, gy, g, xcfl, ycfl, chunk, rb, wpe, s)
+               : tune2_rb<double, false>(p, c, pitch, gy, g, xcfl, ycfl, chunk, rb, wpe, s);
+}
+
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(heat_naive_f32_o8, 256, heat_naive_kernel<float, 8>);
 CME_REGISTER_KERNEL(heat_lds_f32_o8, 256, heat_lds_kernel<float, 8, 32, 1>);
 CME_REGISTER_KERNEL(heat_stream_f32_o8, 256, heat_stream_kernel<float, 8, 4>);
-CME_REGISTER_KERNEL(heat_stream2_f32_o8, 256, heat_stream2_kernel<float, 8, 4>);
-CME_REGISTER_KERNEL(heat_stream2_f64_o8, 256, heat_stream2_kernel<double, 8, 2>);
+CME_REGISTER_KERNEL(heat_stream2_f32_o8, 256, heat_stream2_kernel<float, 8, 4, false>);
+CME_REGISTER_KERNEL(heat_stream2_fma_f32_o8, 256, heat_stream2_kernel<float, 8, 4, true>);
+CME_REGISTER_KERNEL(heat_stream2_f64_o8, 256, heat_stream2_kernel<double, 8, 2, false>);

@@ -9,6 +9,8 @@
 // the reference's 10-ULP tolerance.
 #pragma once
 
+#include <cmath>
+
 #if defined(__HIPCC__)
 #define CME_HD __host__ __device__ __forceinline__
 #else
@@ -46,6 +48,63 @@ CME_HD T heat_update(T c, const T* xm, const T* xp, const T* ym, const T* yp, T 
     T dx = heat_d2<ORDER>(c, xm, xp);
     T dy = heat_d2<ORDER>(c, ym, yp);
     return c + xcfl * dx + ycfl * dy;
+}
+
+// ---- FMA-contracted form ------------------------------------------------
+// The same left-to-right sums with every multiply-add fused -- what nvcc
+// generates for the reference's GPU kernels by default (-fmad=true), and why
+// the reference checks GPU vs CPU within 10 ULP. Explicit fma() calls are
+// correctly rounded on both sides, so the GPU result is bitwise equal to the
+// CPU oracle's FMA mode. 20 flops-instructions per point at order 8 instead
+// of 38.
+template <typename T>
+CME_HD T fmaT(T a, T b, T c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (sizeof(T) == 4)
+        return __builtin_fmaf(a, b, c);
+    else
+        return __builtin_fma(a, b, c);
+#else
+    return std::fma(a, b, c);
+#endif
+}
+
+template <int ORDER, typename T>
+CME_HD T heat_d2_fma(T c, const T* m, const T* p) {
+    if constexpr (ORDER == 2) {
+        return fmaT<T>(T(-2), c, p[0] + m[0]);
+    } else if constexpr (ORDER == 4) {
+        T t = -p[1];
+        t = fmaT<T>(T(16), p[0], t);
+        t = fmaT<T>(T(-30), c, t);
+        t = fmaT<T>(T(16), m[0], t);
+        return t - m[1];
+    } else {
+        T t = T(-9) * p[3];
+        t = fmaT<T>(T(128), p[2], t);
+        t = fmaT<T>(T(-1008), p[1], t);
+        t = fmaT<T>(T(8064), p[0], t);
+        t = fmaT<T>(T(-14350), c, t);
+        t = fmaT<T>(T(8064), m[0], t);
+        t = fmaT<T>(T(-1008), m[1], t);
+        t = fmaT<T>(T(128), m[2], t);
+        return fmaT<T>(T(-9), m[3], t);
+    }
+}
+
+template <int ORDER, typename T>
+CME_HD T heat_update_fma(T c, const T* xm, const T* xp, const T* ym, const T* yp, T xcfl, T ycfl) {
+    const T dx = heat_d2_fma<ORDER>(c, xm, xp);
+    const T dy = heat_d2_fma<ORDER>(c, ym, yp);
+    return fmaT<T>(ycfl, dy, fmaT<T>(xcfl, dx, c));
+}
+
+template <int ORDER, bool FMA, typename T>
+CME_HD T heat_update_sel(T c, const T* xm, const T* xp, const T* ym, const T* yp, T xcfl, T ycfl) {
+    if constexpr (FMA)
+        return heat_update_fma<ORDER>(c, xm, xp, ym, yp, xcfl, ycfl);
+    else
+        return heat_update<ORDER>(c, xm, xp, ym, yp, xcfl, ycfl);
 }
 
 }  // namespace cme

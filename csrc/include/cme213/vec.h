@@ -56,19 +56,20 @@ __device__ __forceinline__ void store4(T* p, const V4<T>& r) {
     }
 }
 
-// Whole-vector lane shifts: lane i receives lane i-1 (shr) / i+1 (shl).
+// Whole-vector lane shifts: lane i receives lane i-1 (shr) / i+1 (shl); the
+// edge lane (0 for shr, 63 for shl) receives 0.
 template <typename T>
 __device__ __forceinline__ V4<T> wave_shr1(const V4<T>& x) {
     V4<T> r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r.v[j] = dpp_move<kDppWaveShr1>(x.v[j], x.v[j]);
+    for (int j = 0; j < 4; ++j) r.v[j] = dpp_shift<kDppWaveShr1>(x.v[j]);
     return r;
 }
 template <typename T>
 __device__ __forceinline__ V4<T> wave_shl1(const V4<T>& x) {
     V4<T> r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r.v[j] = dpp_move<kDppWaveShl1>(x.v[j], x.v[j]);
+    for (int j = 0; j < 4; ++j) r.v[j] = dpp_shift<kDppWaveShl1>(x.v[j]);
     return r;
 }
 

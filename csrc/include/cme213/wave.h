@@ -30,6 +30,13 @@ __device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t src) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, CTRL, ROW_MASK, BANK_MASK, false);
 }
 
+// Pure lane shift: lanes with no source lane read 0 (bound_ctrl) and there is
+// no `old` operand, so the compiler need not copy the source register first.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_shift_u32(uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)src, CTRL, 0xf, 0xf, true);
+}
+
 template <typename T> struct Bits;
 template <> struct Bits<float> { using U = uint32_t; };
 template <> struct Bits<int> { using U = uint32_t; };
@@ -150,6 +157,19 @@ __device__ __forceinline__ T block_reduce(T v, T* lds, Op op = Op()) {
     for (int i = 0; i < NW; ++i) run = op(run, lds[i]);
     __syncthreads();
     return run;
+}
+
+template <int CTRL, typename T>
+__device__ __forceinline__ T dpp_shift(T src) {
+    using U = typename Bits<T>::U;
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, dpp_shift_u32<CTRL>(__builtin_bit_cast(U, src)));
+    } else {
+        const U s = __builtin_bit_cast(U, src);
+        const uint32_t lo = dpp_shift_u32<CTRL>((uint32_t)s);
+        const uint32_t hi = dpp_shift_u32<CTRL>((uint32_t)(s >> 32));
+        return __builtin_bit_cast(T, ((U)hi << 32) | lo);
+    }
 }
 
 }  // namespace cme

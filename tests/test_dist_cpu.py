@@ -7,7 +7,7 @@ import torch
 from dist_util import run_ranks
 
 
-def _heat_rank(rank, world, method, sync, order, tblock=1):
+def _heat_rank(rank, world, method, sync, order, tblock=1, fma=False):
     import cme213x
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.parallel.comm import TorchComm
@@ -15,7 +15,7 @@ def _heat_rank(rank, world, method, sync, order, tblock=1):
 
     p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   sync=sync, flavor="hw5")
-    sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive", tblock=tblock)
+    sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive", tblock=tblock, fma=fma)
     # non-uniform initial condition (same on every rank, by global coords)
     for s in sim.subs.values():
         g, b = s.grid, s.blk
@@ -30,14 +30,14 @@ def _heat_rank(rank, world, method, sync, order, tblock=1):
     return (s.blk.x0, s.blk.y0, s.grid.state()[B:B + s.blk.ny, B:B + s.blk.nx])
 
 
-def _single(method, order, sync):
+def _single(method, order, sync, fma=False):
     import cme213x
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.utils.params import SimParams
 
     p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   sync=sync, flavor="hw5")
-    sim = DistHeat(p, None, torch.float64, "cpu", variant="naive")
+    sim = DistHeat(p, None, torch.float64, "cpu", variant="naive", fma=fma)
     g = sim.subs[0].grid
     B = g.B
     yy, xx = np.meshgrid(np.arange(p.ny), np.arange(p.nx), indexing="ij")
@@ -50,9 +50,10 @@ def _single(method, order, sync):
                          [(1, True, 8, 2, 1), (1, False, 4, 2, 1), (2, False, 8, 4, 1), (2, True, 2, 4, 1),
                           (1, False, 8, 3, 2), (1, True, 4, 2, 2), (2, False, 8, 4, 2), (2, True, 2, 4, 2),
                           (2, False, 4, 6, 2)])
-def test_dist_heat_matches_single(method, sync, order, world, tblock):
-    parts = run_ranks(_heat_rank, world, (method, sync, order, tblock))
-    ref = _single(method, order, sync)
+@pytest.mark.parametrize("fma", [False, True])
+def test_dist_heat_matches_single(method, sync, order, world, tblock, fma):
+    parts = run_ranks(_heat_rank, world, (method, sync, order, tblock, fma))
+    ref = _single(method, order, sync, fma)
     for x0, y0, st in parts:
         np.testing.assert_array_equal(st, ref[y0:y0 + st.shape[0], x0:x0 + st.shape[1]])
 

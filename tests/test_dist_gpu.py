@@ -22,8 +22,8 @@ def _setup_single():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sync", [True, False])
-@pytest.mark.parametrize("tblock", [1, 2])
-def test_native_loop_world1(gpu, sync, tblock):
+@pytest.mark.parametrize("tblock,fma", [(1, False), (2, False), (2, True)])
+def test_native_loop_world1(gpu, sync, tblock, fma):
     import torch.distributed as dist
 
     from cme213x.models.heat2d import HeatGrid
@@ -34,12 +34,12 @@ def test_native_loop_world1(gpu, sync, tblock):
 
     _setup_single()
     p = SimParams(nx=300, ny=211, order=8, iters=7, sync=sync, flavor="hw5")
-    sim = DistHeat(p, TorchComm(), torch.float32, gpu, tblock=tblock)
+    sim = DistHeat(p, TorchComm(), torch.float32, gpu, tblock=tblock, fma=fma)
     rc = NativeRccl()
     sim.run_native(7, rc)
     torch.cuda.synchronize()
     ref = HeatGrid(p, torch.float32, gpu)
-    ref.run(7, "stream")
+    ref.run(7, "stream_fma" if fma else "stream")
     B = p.border
     assert np.array_equal(sim.gather_global()[B:-B, B:-B], ref.state().astype(np.float64)[B:-B, B:-B])
     x = torch.arange(10, dtype=torch.float32, device=gpu)
@@ -52,7 +52,8 @@ def test_native_loop_world1(gpu, sync, tblock):
 @pytest.mark.gpu
 @pytest.mark.parametrize("method,world,sync", [(1, 4, False), (2, 4, False), (2, 6, True), (1, 3, True)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype):
+@pytest.mark.parametrize("fma", [False, True])
+def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype, fma):
     """Several subdomains in one process on the GPU (halo exchange = device
     copies): the fused two-step kernel on interior/border regions with the
     step-1 region grown into 2B-deep halos must reproduce the single-grid CPU
@@ -62,8 +63,8 @@ def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype):
 
     p = SimParams(nx=333, ny=270, order=8, iters=7, sync=sync, grid_method=method, ic=5.0,
                   bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
-    ref = DistHeat(p, None, dtype, "cpu", variant="naive")
-    sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=2)
+    ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)
+    sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=2, fma=fma)
     for d in (ref, sim):
         for s in d.subs.values():
             g, b = s.grid, s.blk

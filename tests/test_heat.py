@@ -144,17 +144,44 @@ def test_gpu_stream2_temporal_blocking_bitwise(gpu, order, dtype, iters):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("variant,iters", [("stream_fma", 3), ("stream2_fma", 1), ("stream2_fma", 4), ("stream2_fma", 7)])
+def test_gpu_fma_variants_bitwise_vs_fma_oracle(gpu, order, dtype, variant, iters):
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, dtype)
+    g = _rand_grid(p, dtype, gpu)
+    c.run(iters, "fma")
+    g.run(iters, variant)
+    torch.cuda.synchronize()
+    d = ulp_distance(c.state(), g.state())
+    assert int(d.max()) == 0, f"max ulp {int(d.max())}"
+
+
+def test_fma_oracle_within_reference_tolerance():
+    """The FMA-contracted stencil stays within the reference's 10-ULP
+    criterion of the exact oracle (hw2 checkErrors)."""
+    p = SimParams(nx=120, ny=90, order=8)
+    a = _rand_grid(p, torch.float32)
+    b = _rand_grid(p, torch.float32)
+    a.run(10, "naive")
+    b.run(10, "fma")
+    assert check_errors(a.state(), b.state(), p.border) == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("region", [(4, 300, 4, 100), (9, 250, 17, 77), (130, 131, 5, 200), (8, 292, 8, 242)])
 @pytest.mark.parametrize("chunk", [0, 8, 12])
-def test_gpu_stream2_subregion(gpu, region, chunk):
+@pytest.mark.parametrize("fma", [False, True])
+def test_gpu_stream2_subregion(gpu, region, chunk, fma):
     from cme213x.ops.stencil import heat_run
     p = SimParams(nx=300, ny=250, order=8)
     c = _rand_grid(p, torch.float32)
     g = _rand_grid(p, torch.float32, gpu)
     ca, cb = c.buf[0].clone(), c.buf[0].clone()
     ga, gb = g.buf[0].clone(), g.buf[0].clone()
-    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 4)
-    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 4, "stream2", chunk)
+    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 4, "fma" if fma else "naive")
+    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 4, "stream2_fma" if fma else "stream2", chunk)
     torch.cuda.synchronize()
     assert torch.equal(oc, og.cpu())
 
