@@ -37,7 +37,7 @@ _CT = {
 }
 
 # name -> argument signature (return type is always int)
-HIP_PROTOS: dict[str, str] = {}
+HIP_PROTOS: dict[str, str] = {"cme_device_sync": ""}
 CPU_PROTOS: dict[str, str] = {}
 
 
@@ -116,8 +116,27 @@ def ptr(t: torch.Tensor) -> int:
     return t.data_ptr()
 
 
+# Debug / observability switches (read once):
+#   CME_SYNC_CHECK=1  synchronise the device after every native HIP call and
+#                     raise at the call that faulted (the reference's
+#                     check_launch, mp1-util.h:8-18, as an opt-in; also the
+#                     HIP_LAUNCH_BLOCKING-style race triage mode of SURVEY §5)
+#   CME_TRACE=1       wrap every native HIP call in a roctx range named after
+#                     the entry point (rocprofv3 --marker-trace shows them)
+SYNC_CHECK = os.environ.get("CME_SYNC_CHECK", "0") not in ("", "0")
+TRACE = os.environ.get("CME_TRACE", "0") not in ("", "0")
+
+
 def call_hip(name: str, *args) -> None:
-    check(_fn("hip", name)(*args), name, "hip")
+    if TRACE:
+        torch.cuda.nvtx.range_push(name)
+    try:
+        check(_fn("hip", name)(*args), name, "hip")
+        if SYNC_CHECK:
+            check(_fn("hip", "cme_device_sync")(), f"{name} (asynchronous failure, CME_SYNC_CHECK)", "hip")
+    finally:
+        if TRACE:
+            torch.cuda.nvtx.range_pop()
 
 
 def call_cpu(name: str, *args) -> None:

@@ -1,1 +1,1 @@
-from . import comm, decomp, collectives, rccl  # noqa: F401
+from . import comm, decomp, collectives, rccl, dist_scan  # noqa: F401

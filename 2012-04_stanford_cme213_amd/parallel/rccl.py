@@ -17,6 +17,8 @@ _ext.proto(_ext.HIP_PROTOS, "cme_rccl_destroy", "p")
 _ext.proto(_ext.HIP_PROTOS, "cme_rccl_allreduce", "pppqiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_rccl_allgather", "pppqip")
 _ext.proto(_ext.HIP_PROTOS, "cme_rccl_p2p", "pippppip")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_async_error", "pp")
+_ext.proto(_ext.HIP_PROTOS, "cme_rccl_abort", "p")
 
 _DT = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4}
 _OP = {"sum": 0, "max": 1, "min": 2, "prod": 3}
@@ -63,6 +65,20 @@ class NativeRccl:
         _ext.call_hip("cme_rccl_p2p", self.handle, n, ctypes.addressof(peers), ctypes.addressof(sends),
                       ctypes.addressof(ptrs), ctypes.addressof(cnts), _DT[ops[0][1].dtype],
                       _ext.stream_ptr(ops[0][1].device))
+
+    def check(self) -> None:
+        """Raise if the communicator reported an asynchronous error (and
+        abort it, so no collective can hang on a dead peer)."""
+        err = ctypes.c_int(0)
+        _ext.call_hip("cme_rccl_async_error", self.handle, ctypes.addressof(err))
+        if err.value != 0:
+            self.abort()
+            raise RuntimeError(f"RCCL asynchronous error {err.value}; communicator aborted")
+
+    def abort(self) -> None:
+        if self.handle:
+            _ext.call_hip("cme_rccl_abort", self.handle)
+            self.handle = None
 
     def close(self) -> None:
         if self.handle:

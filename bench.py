@@ -140,6 +140,8 @@ def main() -> int:
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     comm.barrier()
+    if rccl is not None:
+        rccl.check()  # surface asynchronous RCCL failures instead of reporting a number
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     comm.allreduce_(elapsed, "max")
     secs = float(elapsed.item())

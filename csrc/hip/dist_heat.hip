@@ -55,6 +55,21 @@ CME_EXPORT int cme_rccl_init(void** comm, int nranks, const void* id128, int ran
     return 0;
 }
 
+// Failure detection: poll the communicator's asynchronous error state (a
+// peer died, a network/xGMI error) and abort it so pending collectives return
+// instead of hanging (SURVEY §5 "communicator-abort path").
+CME_EXPORT int cme_rccl_async_error(void* comm, int* err) {
+    ncclResult_t r;
+    NCCL_TRY(ncclCommGetAsyncError((ncclComm_t)comm, &r));
+    *err = (int)r;
+    return 0;
+}
+
+CME_EXPORT int cme_rccl_abort(void* comm) {
+    NCCL_TRY(ncclCommAbort((ncclComm_t)comm));
+    return 0;
+}
+
 CME_EXPORT int cme_rccl_destroy(void* comm) {
     NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
     return 0;

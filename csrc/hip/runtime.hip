@@ -18,6 +18,12 @@ CME_EXPORT int cme_device_info(int dev, int* cus, int* lds_per_block, int* wave,
 
 CME_EXPORT int cme_sync(void* stream) { return (int)hipStreamSynchronize(as_stream(stream)); }
 
+// Device-wide barrier + sticky-error check (CME_SYNC_CHECK debug mode).
+CME_EXPORT int cme_device_sync() {
+    CME_TRY(hipDeviceSynchronize());
+    return (int)hipGetLastError();
+}
+
 // -------------------------------------------------------------- registry
 // Resource / occupancy report for the registered kernels: the MI355X answer
 // to the reference's CUDA Occupancy Calculator spreadsheet and `ptxas -v`

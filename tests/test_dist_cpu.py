@@ -180,3 +180,102 @@ def test_p2p_collectives_gloo():
         assert b == [2.0] * 3
         if rank == 1:
             assert r == sum(range(1, world + 1))
+
+
+def _dist_scan_rank(rank, world, seed):
+    import cme213x
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.parallel.dist_scan import dist_scan, dist_segmented_scan
+
+    rng = np.random.default_rng(seed)
+    n = 10_007
+    x = rng.integers(-5, 6, n).astype(np.float32)  # small integers: fp32 sums are exact
+    flags = (rng.random(n) < 0.001).astype(np.uint8)
+    flags[0] = 1
+    cuts = sorted(rng.choice(np.arange(1, n), world - 1, replace=False).tolist())
+    bounds = [0] + cuts + [n]
+    lo, hi = bounds[rank], bounds[rank + 1]
+    c = TorchComm()
+    inc = dist_scan(torch.from_numpy(x[lo:hi].copy()), c)
+    exc = dist_scan(torch.from_numpy(x[lo:hi].copy()), c, exclusive=True)
+    seg = dist_segmented_scan(torch.from_numpy(x[lo:hi].copy()), torch.from_numpy(flags[lo:hi].copy()), c)
+    return lo, hi, inc.numpy(), exc.numpy(), seg.numpy()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_dist_scan_gloo(world):
+    rng = np.random.default_rng(7)
+    n = 10_007
+    x = rng.integers(-5, 6, n).astype(np.float32)
+    flags = (rng.random(n) < 0.001).astype(np.uint8)
+    flags[0] = 1
+    inc = np.cumsum(x.astype(np.float64))
+    seg = np.empty(n)
+    acc = 0.0
+    for i in range(n):
+        acc = x[i] if flags[i] else acc + x[i]
+        seg[i] = acc
+    for lo, hi, yi, ye, ys in run_ranks(_dist_scan_rank, world, (7,)):
+        np.testing.assert_array_equal(yi, inc[lo:hi])
+        np.testing.assert_array_equal(ye, (inc - x)[lo:hi])
+        np.testing.assert_array_equal(ys, seg[lo:hi])
+
+
+def _dist_spmvscan_rank(rank, world):
+    import cme213x
+    from cme213x.models.spmv_scan import generate
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.parallel.dist_scan import DistSpmvScan
+
+    prob = generate(20_000, 40, 500, 4, seed=3)  # few long segments: most straddle shards
+    a, xx, f = DistSpmvScan.shard(prob, rank, world)
+    d = DistSpmvScan(a, xx, f, TorchComm())
+    out = d.run(prob.iters)
+    n = prob.n
+    return n * rank // world, out.numpy()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_spmv_scan_gloo(world):
+    from cme213x.models.spmv_scan import errors, generate, reference_solution
+
+    prob = generate(20_000, 40, 500, 4, seed=3)
+    ref = reference_solution(prob)
+    parts = sorted(run_ranks(_dist_spmvscan_rank, world), key=lambda t: t[0])
+    b = np.concatenate([p for _, p in parts])
+    e = errors(ref, b)
+    assert e["relL2"] < 1e-5, e
+
+
+def _ckpt_rank(rank, world, directory, tblock):
+    import cme213x
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=64, ny=48, iters=8, order=4, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=2, sync=False,
+                  flavor="hw5")
+    c = TorchComm()
+    full = DistHeat(p, c, torch.float64, "cpu", variant="naive", tblock=tblock)
+    for s in full.subs.values():
+        g, b = s.grid, s.blk
+        yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+        g.buf[:, g.H:g.H + b.ny, g.H:g.H + b.nx] = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0)
+    full.exchange(full._cur()).wait()
+    full.run(5)
+    full.checkpoint(directory)
+    full.run(6)
+    # a fresh solver resumes from the checkpoint and must land on the same state
+    resumed = DistHeat(p, c, torch.float64, "cpu", variant="naive", tblock=tblock)
+    resumed.restore(directory)
+    assert resumed.iteration == 5
+    resumed.run(6)
+    a = next(iter(full.subs.values())).grid
+    b = next(iter(resumed.subs.values())).grid
+    B = a.B
+    return bool(np.array_equal(a.state()[B:-B, B:-B], b.state()[B:-B, B:-B]))
+
+
+@pytest.mark.parametrize("tblock", [1, 2])
+def test_dist_heat_checkpoint_restart_gloo(tmp_path, tblock):
+    assert all(run_ranks(_ckpt_rank, 4, (str(tmp_path), tblock)))

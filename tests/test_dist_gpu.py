@@ -45,6 +45,7 @@ def test_native_loop_world1(gpu, sync, tblock, fma):
     x = torch.arange(10, dtype=torch.float32, device=gpu)
     rc.allreduce_(x)
     assert torch.equal(x.cpu(), torch.arange(10, dtype=torch.float32))
+    rc.check()  # no asynchronous communicator error
     rc.close()
     dist.destroy_process_group()
 
