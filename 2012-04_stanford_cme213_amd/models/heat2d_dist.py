@@ -28,6 +28,7 @@ are used, so non-uniform initial conditions are correct.
 """
 from __future__ import annotations
 
+import ctypes
 import time
 
 import numpy as np
@@ -38,6 +39,16 @@ from ..parallel.comm import Comm, LoopbackComm, P2P, Pending
 from ..parallel.decomp import Block, decompose
 from ..utils.params import SimParams
 from .heat2d import HeatGrid
+
+
+class SubDesc(ctypes.Structure):
+    """Mirror of ``SubDesc`` in ``csrc/hip/dist_heat.hip`` (one subdomain of
+    the native distributed loop)."""
+    _fields_ = [("buf", ctypes.c_void_p * 2), ("pitch", ctypes.c_int), ("gy", ctypes.c_int),
+                ("interior", ctypes.c_void_p), ("n_int", ctypes.c_int), ("border", ctypes.c_void_p),
+                ("n_b", ctypes.c_int), ("ext", ctypes.c_void_p), ("rows", ctypes.c_void_p),
+                ("n_rows", ctypes.c_int), ("blks", ctypes.c_void_p), ("n_blks", ctypes.c_int),
+                ("stage", ctypes.c_void_p), ("rank", ctypes.c_int)]
 
 
 class _Sub:
@@ -254,10 +265,9 @@ class DistHeat:
         self.iteration += 2
 
     # -- native loop (RCCL + HIP, no per-step Python) ---------------------
-    def _native_plan(self):
-        if getattr(self, "_plan", None) is not None:
-            return self._plan
-        (r, s), = self.subs.items()
+    def _sub_plan(self, r: int, s: _Sub) -> dict:
+        """Index plan of one subdomain for the native loop (element offsets
+        and regions in its own grid coordinates)."""
         g, b = s.grid, s.blk
         H, ny, nx, pitch = g.H, g.ny, g.nx, g.pitch
         D = self.tblock * g.B
@@ -282,7 +292,7 @@ class DistHeat:
             rx, ry = s.corner_origin(dx, dy, False)
             cols.append((peer, sx, sy, rx, ry, H, H))
         stage_elems = 2 * sum(c[5] * c[6] for c in cols)
-        plan = {
+        return {
             "interior": torch.tensor(np.array(interior, dtype=np.int32).reshape(-1, 4)),
             "border": torch.tensor(np.array(border, dtype=np.int32).reshape(-1, 4)),
             "ext": torch.tensor(np.array(_ext_region(s), dtype=np.int32)),
@@ -290,35 +300,59 @@ class DistHeat:
             "cols": torch.tensor(np.array(cols, dtype=np.int32).reshape(-1, 7)),
             "stage": torch.empty(max(stage_elems, 1), dtype=g.dtype, device=g.device),
         }
-        self._plan = plan
-        return plan
 
-    def run_native(self, iters: int, rccl, sync: bool | None = None) -> None:
-        """``iters`` timesteps in ONE native call (RCCL P2P halo exchange on a
-        communication stream, interior/exchange overlap in async mode; with
-        ``tblock=2`` each exchange of 2B-deep halos feeds two timesteps done
-        in one HBM pass). ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl`."""
+    def _native_plan(self):
+        """ctypes array of SubDesc (one per local subdomain) + the tensors it
+        points into (kept alive with it)."""
+        if getattr(self, "_plan", None) is not None:
+            return self._plan
+        plans = {r: self._sub_plan(r, s) for r, s in self.subs.items()}
+        arr = (SubDesc * len(plans))()
+        for i, (r, s) in enumerate(self.subs.items()):
+            pl, g = plans[r], s.grid
+            d = arr[i]
+            d.buf[0], d.buf[1] = g.buf[0].data_ptr(), g.buf[1].data_ptr()
+            d.pitch, d.gy = g.pitch, g.gy
+            d.interior, d.n_int = pl["interior"].data_ptr(), pl["interior"].shape[0]
+            d.border, d.n_b = pl["border"].data_ptr(), pl["border"].shape[0]
+            d.ext = pl["ext"].data_ptr()
+            d.rows, d.n_rows = pl["rows"].data_ptr(), pl["rows"].shape[0]
+            d.blks, d.n_blks = pl["cols"].data_ptr(), pl["cols"].shape[0]
+            d.stage = pl["stage"].data_ptr()
+            d.rank = r
+        self._plan = {"subs": arr, "plans": plans}
+        return self._plan
+
+    def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None) -> None:
+        """``iters`` timesteps in ONE native call (``cme_heat_dist_run``):
+        border strips on their own stream, the halo exchange posted as soon
+        as they finish, the deep interior overlapping both; with ``tblock=2``
+        each exchange of 2B-deep halos feeds two timesteps done in one HBM
+        pass. ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl` (one
+        subdomain per process); ``None`` = loopback transport, every
+        neighbour being another local subdomain (device copies) -- the same
+        stream/event schedule, testable on one GPU. ``transport=2`` skips
+        the exchange (compute-schedule benchmarking only)."""
         import ctypes
 
         from .. import _ext
 
-        if len(self.subs) != 1:
-            raise ValueError("native loop: one subdomain per process")
+        if rccl is not None and len(self.subs) != 1:
+            raise ValueError("RCCL transport: one subdomain per process")
         self.finish()
         sync = self.p.sync if sync is None else sync
         plan = self._native_plan()
-        (r, s), = self.subs.items()
-        g = s.grid
+        g0 = next(iter(self.subs.values())).grid
         cur_out = ctypes.c_int(0)
-        _ext.call_hip("cme_heat_dist_run", rccl.handle, g.buf[0].data_ptr(), g.buf[1].data_ptr(), g.pitch, g.gy,
-                      plan["interior"].data_ptr(), plan["interior"].shape[0], plan["border"].data_ptr(),
-                      plan["border"].shape[0], plan["ext"].data_ptr(), self.tblock, int(self.fma),
-                      plan["rows"].data_ptr(), plan["rows"].shape[0],
-                      plan["cols"].data_ptr(), plan["cols"].shape[0], plan["stage"].data_ptr(),
-                      0 if g.dtype == torch.float32 else 1, g.order, g.xcfl, g.ycfl, iters, g.cur, int(sync), 0,
-                      ctypes.addressof(cur_out), _ext.stream_ptr(g.device))
-        g.cur = cur_out.value
-        g.iteration += iters
+        if transport is None:
+            transport = 0 if rccl is not None else 1
+        _ext.call_hip("cme_heat_dist_run", transport, rccl.handle if rccl is not None else None,
+                      ctypes.addressof(plan["subs"]), len(self.subs), 0 if g0.dtype == torch.float32 else 1,
+                      g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock, int(self.fma),
+                      ctypes.addressof(cur_out), _ext.stream_ptr(g0.device))
+        for s in self.subs.values():
+            s.grid.cur = cur_out.value
+            s.grid.iteration += iters
         self.iteration += iters
 
     def finish(self) -> None:

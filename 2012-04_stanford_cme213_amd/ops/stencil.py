@@ -18,9 +18,9 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiipp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiippiffiip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiippiddiip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "pppiipipipiipipipiiddiiiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiipipiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiipipiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -88,7 +88,7 @@ def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, i
     r = (ctypes.c_int * 4)(*map(int, region))
     e = (ctypes.c_int * 4)(*map(int, ext))
     name = "cme_heat_step2_f64" if prev.dtype == torch.float64 else "cme_heat_step2_f32"
-    _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), ctypes.addressof(e),
+    _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), 1, ctypes.addressof(e),
                   order, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
 
 

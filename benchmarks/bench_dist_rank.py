@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Compute side of the strong-scaling flagship on ONE GPU: time one rank's
+per-step schedule (deep interior + border strips, two fused steps per pass)
+for the subdomain an N-GPU run gives each rank, with the halo exchange
+replaced by a no-op. ms/step x N vs the N=1 time shows how much of ideal
+strong scaling the compute schedule itself keeps (launch overhead, thin
+border strips, halo redundancy) -- independent of RCCL.
+
+    python benchmarks/bench_dist_rank.py [--n 16384] [--world 1 2 4 8] [--method 1]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--world", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--method", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--fma", type=int, default=1)
+    ap.add_argument("--native", type=int, default=1, help="1: native loop (null transport); 0: Python loop")
+    args = ap.parse_args()
+    import torch
+
+    import cme213x
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import Comm, Pending
+    from cme213x.utils.params import SimParams
+
+    class NullComm(Comm):
+        """Pretends to be rank r of W; exchanges complete immediately."""
+
+        def __init__(self, rank, size):
+            self.rank, self.size = rank, size
+
+        def exchange(self, ops):
+            return Pending()
+
+        def allreduce_(self, t, op="sum"):
+            return t
+
+        def barrier(self):
+            pass
+
+    base = None
+    for w in args.world:
+        rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
+        p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=False, flavor="hw5")
+        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=2, fma=bool(args.fma))
+
+        def run(k):
+            if args.native:
+                sim.run_native(k, transport=2)
+            else:
+                sim.run(k)
+
+        run(10)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        run(args.steps)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.steps
+        base = base or ms * w
+        print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native,
+                          "ms_per_step": round(ms, 4),
+                          "compute_scaling_eff": round(base / (ms * w), 3)}), flush=True)
+        del sim
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,10 +21,12 @@ extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int 
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream);
 extern "C" int cme_heat_step_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, double xcfl, double ycfl, int chunk, void* stream);
-extern "C" int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, float xcfl, float ycfl, int chunk, int fma, void* stream);
-extern "C" int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, double xcfl, double ycfl, int chunk, int fma, void* stream);
+extern "C" int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, float xcfl, float ycfl, int chunk, int fma,
+                                  void* stream);
+extern "C" int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, double xcfl, double ycfl, int chunk, int fma,
+                                  void* stream);
 
 #define CME_TRY_INT(expr)                 \
     do {                                  \
@@ -150,27 +152,6 @@ __global__ __launch_bounds__(256) void unpack_block_kernel(T* __restrict__ g, in
     g[(size_t)(y0 + r) * pitch + x0 + c] = stage[i];
 }
 
-struct DistCtx {
-    int dev = -1;
-    hipStream_t comm_stream = nullptr;
-    hipEvent_t ev_compute = nullptr, ev_comm = nullptr;
-};
-
-int get_ctx(DistCtx** out) {
-    static DistCtx ctx[16];
-    int dev;
-    CME_TRY(hipGetDevice(&dev));
-    DistCtx& c = ctx[dev & 15];
-    if (c.dev != dev) {
-        CME_TRY(hipStreamCreateWithFlags(&c.comm_stream, hipStreamNonBlocking));
-        CME_TRY(hipEventCreateWithFlags(&c.ev_compute, hipEventDisableTiming));
-        CME_TRY(hipEventCreateWithFlags(&c.ev_comm, hipEventDisableTiming));
-        c.dev = dev;
-    }
-    *out = &c;
-    return 0;
-}
-
 // single step: streaming kernel, exact (variant 2) or FMA (variant 6)
 template <typename T>
 int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T xcfl, T ycfl, int fma,
@@ -187,53 +168,115 @@ int step_region<double>(const double* p, double* c, int pitch, int gy, const int
     return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
 }
 
+// two-step pass over n (<= 4) regions in one launch
 template <typename T>
-int step2_region(const T* p, T* c, int pitch, int gy, const int* r, const int* ext, int order, T xcfl, T ycfl,
-                 int fma, hipStream_t s);
+int step2_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, T xcfl,
+                  T ycfl, int fma, hipStream_t s);
 
 template <>
-int step2_region<float>(const float* p, float* c, int pitch, int gy, const int* r, const int* ext, int order,
-                        float xcfl, float ycfl, int fma, hipStream_t s) {
-    return cme_heat_step2_f32(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, fma, (void*)s);
+int step2_regions<float>(const float* p, float* c, int pitch, int gy, const int* r, int n, const int* ext, int order,
+                         float xcfl, float ycfl, int fma, hipStream_t s) {
+    return cme_heat_step2_f32(p, c, pitch, gy, r, n, ext, order, xcfl, ycfl, 0, fma, (void*)s);
 }
 template <>
-int step2_region<double>(const double* p, double* c, int pitch, int gy, const int* r, const int* ext, int order,
-                         double xcfl, double ycfl, int fma, hipStream_t s) {
-    return cme_heat_step2_f64(p, c, pitch, gy, r, ext, order, xcfl, ycfl, 0, fma, (void*)s);
+int step2_regions<double>(const double* p, double* c, int pitch, int gy, const int* r, int n, const int* ext,
+                          int order, double xcfl, double ycfl, int fma, hipStream_t s) {
+    return cme_heat_step2_f64(p, c, pitch, gy, r, n, ext, order, xcfl, ycfl, 0, fma, (void*)s);
 }
 
-// Exchange plan for buffer `g`:
-//   rows[i*4 + 0..3]  = {peer, send_off, recv_off, count}  (element offsets;
-//                       full pitched rows go straight out of / into the grid)
-//   blks[i*7 + 0..6]  = {peer, send_x, send_y, recv_x, recv_y, rows, width}
-//                       (column halos and, for 2B-deep halos, the corners
-//                       to/from the diagonal peers)
-//   stage: 2 * sum(rows*width) elements (send halves first, then recv halves)
+// ------------------------------------------------------------- distributed loop
+// One descriptor per subdomain owned by this process (1 with RCCL; any number
+// with the loopback transport, where every neighbour lives in this process).
+// Layout must match SubDesc in models/heat2d_dist.py.
+struct SubDesc {
+    void* buf[2];
+    int pitch, gy;
+    const int* interior;  // n_int x {xb, xe, yb, ye}
+    int n_int;
+    const int* border;    // n_b x {xb, xe, yb, ye}
+    int n_b;
+    const int* ext;       // {xb, xe, yb, ye} step-1 region of two-step passes
+    const long long* rows;  // n_rows x {peer, send_off, recv_off, count} (elements)
+    int n_rows;
+    const int* blks;      // n_blks x {peer, send_x, send_y, recv_x, recv_y, rows, width}
+    int n_blks;
+    void* stage;          // RCCL transport: 2 * sum(rows*width) elements
+    int rank;             // global rank of this subdomain
+};
+
 constexpr int kBlk = 7;
+constexpr int kMaxSubs = 64;
 
+// Per-subdomain streams and events. Events for border / interior completion
+// are double-buffered by pass parity so that a pass can wait on the PREVIOUS
+// pass's record while this pass's record is already enqueued.
+struct SubCtx {
+    hipStream_t compute = nullptr, border = nullptr, comm = nullptr;
+    hipEvent_t ev_border[2] = {nullptr, nullptr}, ev_int[2] = {nullptr, nullptr}, ev_comm = nullptr;
+    hipEvent_t ev_start = nullptr;
+};
+
+struct DistCtx {
+    int dev = -1;
+    int nsub = 0;
+    SubCtx sub[kMaxSubs];
+};
+
+int get_ctx(int nsub, DistCtx** out) {
+    static DistCtx ctx[16];
+    int dev;
+    CME_TRY(hipGetDevice(&dev));
+    DistCtx& c = ctx[dev & 15];
+    if (c.dev != dev) {
+        c.dev = dev;
+        c.nsub = 0;
+    }
+    for (int i = c.nsub; i < nsub; ++i) {  // grow lazily, never shrink
+        SubCtx& u = c.sub[i];
+        // border strips and the exchange are on the critical path: their
+        // workgroups are dispatched ahead of the (long) interior kernel's
+        int least = 0, greatest = 0;
+        CME_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        CME_TRY(hipStreamCreateWithFlags(&u.compute, hipStreamNonBlocking));
+        CME_TRY(hipStreamCreateWithPriority(&u.border, hipStreamNonBlocking, greatest));
+        CME_TRY(hipStreamCreateWithPriority(&u.comm, hipStreamNonBlocking, greatest));
+        for (int k = 0; k < 2; ++k) {
+            CME_TRY(hipEventCreateWithFlags(&u.ev_border[k], hipEventDisableTiming));
+            CME_TRY(hipEventCreateWithFlags(&u.ev_int[k], hipEventDisableTiming));
+        }
+        CME_TRY(hipEventCreateWithFlags(&u.ev_comm, hipEventDisableTiming));
+        CME_TRY(hipEventCreateWithFlags(&u.ev_start, hipEventDisableTiming));
+    }
+    if (nsub > c.nsub) c.nsub = nsub;
+    *out = &c;
+    return 0;
+}
+
+// RCCL transport: one grouped send/recv batch on the sub's comm stream.
+// Staged blocks are packed into `stage` first and unpacked after the group.
 template <typename T>
-int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n_rows, const int* blks, int n_blks,
-                  T* stage, ncclDataType_t dt, hipStream_t cs) {
+int post_exchange_rccl(ncclComm_t comm, const SubDesc& d, T* g, ncclDataType_t dt, hipStream_t cs) {
+    T* stage = (T*)d.stage;
     long long total = 0;
-    for (int i = 0; i < n_blks; ++i) total += (long long)blks[i * kBlk + 5] * blks[i * kBlk + 6];
+    for (int i = 0; i < d.n_blks; ++i) total += (long long)d.blks[i * kBlk + 5] * d.blks[i * kBlk + 6];
     long long off = 0;
-    for (int i = 0; i < n_blks; ++i) {
-        const int* c = blks + i * kBlk;
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
         const int cnt = c[5] * c[6];
-        hipLaunchKernelGGL(pack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[1], c[2], c[5],
+        hipLaunchKernelGGL(pack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, d.pitch, c[1], c[2], c[5],
                            c[6], stage + off);
         off += cnt;
     }
     CME_TRY(hipGetLastError());
     NCCL_TRY(ncclGroupStart());
-    for (int i = 0; i < n_rows; ++i) {
-        const long long* r = rows + i * 4;
+    for (int i = 0; i < d.n_rows; ++i) {
+        const long long* r = d.rows + i * 4;
         NCCL_TRY(ncclSend(g + r[1], (size_t)r[3], dt, (int)r[0], comm, cs));
         NCCL_TRY(ncclRecv(g + r[2], (size_t)r[3], dt, (int)r[0], comm, cs));
     }
     off = 0;
-    for (int i = 0; i < n_blks; ++i) {
-        const int* c = blks + i * kBlk;
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
         const long long cnt = (long long)c[5] * c[6];
         NCCL_TRY(ncclSend(stage + off, (size_t)cnt, dt, c[0], comm, cs));
         NCCL_TRY(ncclRecv(stage + total + off, (size_t)cnt, dt, c[0], comm, cs));
@@ -241,10 +284,10 @@ int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n
     }
     NCCL_TRY(ncclGroupEnd());
     off = 0;
-    for (int i = 0; i < n_blks; ++i) {
-        const int* c = blks + i * kBlk;
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
         const int cnt = c[5] * c[6];
-        hipLaunchKernelGGL(unpack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, pitch, c[3], c[4], c[5],
+        hipLaunchKernelGGL(unpack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, d.pitch, c[3], c[4], c[5],
                            c[6], stage + total + off);
         off += cnt;
     }
@@ -252,85 +295,233 @@ int post_exchange(ncclComm_t comm, T* g, int pitch, const long long* rows, int n
     return 0;
 }
 
+int find_sub(const SubDesc* subs, int nsub, int rank) {
+    for (int i = 0; i < nsub; ++i)
+        if (subs[i].rank == rank) return i;
+    return -1;
+}
+
+// Loopback transport: PULL every halo of sub `si` (state k) from the owning
+// neighbour's matching send region with device copies on si's comm stream.
 template <typename T>
-int dist_run(ncclComm_t comm, T* buf0, T* buf1, int pitch, int gy, const int* interior, int n_int, const int* border,
-             int n_b, const int* ext, int tblock, int fma, const long long* rows, int n_rows, const int* cols, int n_cols, T* stage, int order, T xcfl,
-             T ycfl, int iters, int cur, int sync, int exchange_first, int* cur_out, hipStream_t s) {
-    DistCtx* ctx;
-    CME_TRY_INT(get_ctx(&ctx));
-    const ncclDataType_t dt = sizeof(T) == 4 ? ncclFloat32 : ncclFloat64;
-    T* bufs[2] = {buf0, buf1};
-    hipStream_t cs = ctx->comm_stream;
-    if (exchange_first) {  // make halos of the current state valid
-        CME_TRY(hipEventRecord(ctx->ev_compute, s));
-        CME_TRY(hipStreamWaitEvent(cs, ctx->ev_compute, 0));
-        int rc = post_exchange<T>(comm, bufs[cur], pitch, rows, n_rows, cols, n_cols, stage, dt, cs);
-        if (rc) return rc;
-        CME_TRY(hipEventRecord(ctx->ev_comm, cs));
-        CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
+int post_exchange_loopback(const SubDesc* subs, int nsub, int si, int k, hipStream_t cs) {
+    const SubDesc& d = subs[si];
+    T* g = (T*)d.buf[k];
+    for (int i = 0; i < d.n_rows; ++i) {
+        const long long* r = d.rows + i * 4;
+        const int pj = find_sub(subs, nsub, (int)r[0]);
+        if (pj < 0) return (int)hipErrorInvalidValue;
+        const SubDesc& pd = subs[pj];
+        long long src_off = -1;
+        for (int j = 0; j < pd.n_rows; ++j)
+            if (pd.rows[j * 4] == d.rank) src_off = pd.rows[j * 4 + 1];
+        if (src_off < 0) return (int)hipErrorInvalidValue;
+        CME_TRY(hipMemcpyAsync(g + r[2], (T*)pd.buf[k] + src_off, (size_t)r[3] * sizeof(T), hipMemcpyDeviceToDevice,
+                               cs));
     }
-    // tblock == 2: halos are 2B deep, each exchange feeds TWO timesteps computed
-    // in one pass (stream2, intermediate step on region `ext`); odd tails
-    // take one single step (the 2B halo over-satisfies it).
-    for (int it = 0; it < iters;) {
-        const T* p = bufs[cur];
-        T* c = bufs[cur ^ 1];
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
+        const int pj = find_sub(subs, nsub, c[0]);
+        if (pj < 0) return (int)hipErrorInvalidValue;
+        const SubDesc& pd = subs[pj];
+        const int* m = nullptr;
+        for (int j = 0; j < pd.n_blks; ++j)
+            if (pd.blks[j * kBlk] == d.rank) m = pd.blks + j * kBlk;
+        if (!m || m[5] != c[5] || m[6] != c[6]) return (int)hipErrorInvalidValue;
+        const T* src = (const T*)pd.buf[k] + (size_t)m[2] * pd.pitch + m[1];
+        T* dst = g + (size_t)c[4] * d.pitch + c[3];
+        CME_TRY(hipMemcpy2DAsync(dst, (size_t)d.pitch * sizeof(T), src, (size_t)pd.pitch * sizeof(T),
+                                 (size_t)c[6] * sizeof(T), (size_t)c[5], hipMemcpyDeviceToDevice, cs));
+    }
+    return 0;
+}
+
+// peers of sub si that live in this process (loopback dependencies)
+int local_peers(const SubDesc* subs, int nsub, int si, int* out) {
+    int n = 0;
+    const SubDesc& d = subs[si];
+    for (int i = 0; i < d.n_rows; ++i) {
+        const int pj = find_sub(subs, nsub, (int)d.rows[i * 4]);
+        if (pj >= 0) out[n++] = pj;
+    }
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int pj = find_sub(subs, nsub, d.blks[i * kBlk]);
+        if (pj >= 0) out[n++] = pj;
+    }
+    return n;
+}
+
+// The time loop. Per pass i (one or two timesteps), for every sub:
+//   border stream : wait halos of p (own comm event, + pulling neighbours'
+//                   in loopback) and the previous interior; border strips;
+//                   record ev_border[i&1]
+//   comm stream   : wait ev_border[i&1] (+ neighbours' in loopback); post the
+//                   halo exchange of c; record ev_comm
+//   compute stream: wait the previous pass's ev_border; deep interior;
+//                   record ev_int[i&1]
+// so the interior of pass i overlaps both the border strips and the halo
+// exchange of pass i. Sync mode runs everything in order on one stream.
+template <typename T>
+int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int order, T xcfl, T ycfl, int iters,
+             int cur, int sync, int exchange_first, int tblock, int fma, int* cur_out, hipStream_t s) {
+    if (nsub < 1 || nsub > kMaxSubs) return (int)hipErrorInvalidValue;
+    if (transport == 0 && nsub != 1) return (int)hipErrorInvalidValue;
+    // 0 (default): border stream || interior stream; 1: border then interior
+    // on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
+    // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for
+    // re-measuring on other topologies.
+    static const int schedule = [] {
+        const char* e = getenv("CME_DIST_SCHEDULE");
+        return e ? atoi(e) : 0;
+    }();
+    DistCtx* ctx;
+    CME_TRY_INT(get_ctx(nsub, &ctx));
+    const ncclDataType_t dt = sizeof(T) == 4 ? ncclFloat32 : ncclFloat64;
+    int peers[kMaxSubs][16];
+    int npeer[kMaxSubs];
+    for (int si = 0; si < nsub; ++si) {
+        npeer[si] = local_peers(subs, nsub, si, peers[si]);
+        if (transport == 1 && npeer[si] != subs[si].n_rows + subs[si].n_blks) return (int)hipErrorInvalidValue;
+    }
+    auto exchange = [&](int si, int k) -> int {
+        if (transport == 0) return post_exchange_rccl<T>(comm, subs[si], (T*)subs[si].buf[k], dt, ctx->sub[si].comm);
+        if (transport == 1) return post_exchange_loopback<T>(subs, nsub, si, k, ctx->sub[si].comm);
+        return 0;  // transport 2: no exchange (benchmarking the compute schedule)
+    };
+    auto sweep = [&](int si, const int* regs, int n, int k, bool two, hipStream_t st) -> int {
+        const SubDesc& d = subs[si];
+        const T* p = (const T*)d.buf[k];
+        T* c = (T*)d.buf[k ^ 1];
+        if (n == 0) return 0;
+        if (two)  // all regions (e.g. the 2-4 border strips) in ONE launch
+            return step2_regions<T>(p, c, d.pitch, d.gy, regs, n, d.ext, order, xcfl, ycfl, fma, st);
+        for (int i = 0; i < n; ++i) {
+            int rc = step_region<T>(p, c, d.pitch, d.gy, regs + 4 * i, order, xcfl, ycfl, fma, st);
+            if (rc) return rc;
+        }
+        return 0;
+    };
+    // all work starts after what is already queued on the caller's stream
+    for (int si = 0; si < nsub; ++si) {
+        SubCtx& u = ctx->sub[si];
+        CME_TRY(hipEventRecord(u.ev_start, s));
+        CME_TRY(hipStreamWaitEvent(u.compute, u.ev_start, 0));
+        CME_TRY(hipStreamWaitEvent(u.border, u.ev_start, 0));
+        CME_TRY(hipStreamWaitEvent(u.comm, u.ev_start, 0));
+    }
+    if (exchange_first) {  // make the halos of the current state valid
+        for (int si = 0; si < nsub; ++si) CME_TRY_INT(exchange(si, cur));
+        for (int si = 0; si < nsub; ++si) CME_TRY(hipEventRecord(ctx->sub[si].ev_comm, ctx->sub[si].comm));
+        for (int si = 0; si < nsub; ++si)
+            for (int j = 0; j < nsub; ++j) CME_TRY(hipStreamWaitEvent(ctx->sub[si].compute, ctx->sub[j].ev_comm, 0));
+    }
+    int pass = 0;
+    for (int it = 0; it < iters; ++pass) {
         const bool two = tblock == 2 && it + 1 < iters;
-        auto sweep = [&](const int* regs, int n) -> int {
-            for (int i = 0; i < n; ++i) {
-                int rc = two ? step2_region<T>(p, c, pitch, gy, regs + 4 * i, ext, order, xcfl, ycfl, fma, s)
-                             : step_region<T>(p, c, pitch, gy, regs + 4 * i, order, xcfl, ycfl, fma, s);
-                if (rc) return rc;
-            }
-            return 0;
-        };
+        const int par = pass & 1;
         if (sync) {
-            CME_TRY_INT(sweep(interior, n_int));
-            CME_TRY_INT(sweep(border, n_b));
-            CME_TRY(hipEventRecord(ctx->ev_compute, s));
-            CME_TRY(hipStreamWaitEvent(cs, ctx->ev_compute, 0));
-            int rc = post_exchange<T>(comm, c, pitch, rows, n_rows, cols, n_cols, stage, dt, cs);
-            if (rc) return rc;
-            CME_TRY(hipEventRecord(ctx->ev_comm, cs));
-            CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.compute));
+                CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
+            }
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
+                CME_TRY_INT(exchange(si, cur ^ 1));
+                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
+            }
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.compute, u.ev_comm, 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.compute, ctx->sub[peers[si][j]].ev_comm, 0));
+            }
+        } else if (schedule == 1) {
+            // single compute stream: [halos of p] -> border strips -> interior;
+            // the exchange of the new borders overlaps the interior
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.compute, u.ev_comm, 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.compute, ctx->sub[peers[si][j]].ev_comm, 0));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.compute));
+                CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
+            }
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
+                CME_TRY_INT(exchange(si, cur ^ 1));
+                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
+            }
+            for (int si = 0; si < nsub; ++si) {
+                SubCtx& u = ctx->sub[si];
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
+                CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
+            }
         } else {
-            // deep interior needs no ghost cells: overlaps the previous exchange
-            CME_TRY_INT(sweep(interior, n_int));
-            CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));  // halos of p have arrived
-            CME_TRY_INT(sweep(border, n_b));
-            CME_TRY(hipEventRecord(ctx->ev_compute, s));
-            CME_TRY(hipStreamWaitEvent(cs, ctx->ev_compute, 0));
-            int rc = post_exchange<T>(comm, c, pitch, rows, n_rows, cols, n_cols, stage, dt, cs);
-            if (rc) return rc;
-            CME_TRY(hipEventRecord(ctx->ev_comm, cs));
+            for (int si = 0; si < nsub; ++si) {  // border strips of pass i
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.border, u.ev_comm, 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.border, ctx->sub[peers[si][j]].ev_comm, 0));
+                CME_TRY(hipStreamWaitEvent(u.border, u.ev_int[par ^ 1], 0));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.border));
+                CME_TRY(hipEventRecord(u.ev_border[par], u.border));
+            }
+            for (int si = 0; si < nsub; ++si) {  // halo exchange of the new state
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
+                for (int j = 0; j < npeer[si]; ++j)
+                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
+                CME_TRY_INT(exchange(si, cur ^ 1));
+                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
+            }
+            for (int si = 0; si < nsub; ++si) {  // deep interior, overlapping both
+                SubCtx& u = ctx->sub[si];
+                CME_TRY(hipStreamWaitEvent(u.compute, u.ev_border[par ^ 1], 0));
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
+                CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
+            }
         }
         cur ^= 1;
         it += two ? 2 : 1;
     }
-    // leave the compute stream ordered after the last exchange
-    CME_TRY(hipStreamWaitEvent(s, ctx->ev_comm, 0));
+    // the caller's stream resumes after every stream of every sub
+    for (int si = 0; si < nsub; ++si) {
+        SubCtx& u = ctx->sub[si];
+        CME_TRY(hipEventRecord(u.ev_int[0], u.compute));
+        CME_TRY(hipEventRecord(u.ev_border[0], u.border));
+        CME_TRY(hipStreamWaitEvent(s, u.ev_int[0], 0));
+        CME_TRY(hipStreamWaitEvent(s, u.ev_border[0], 0));
+        CME_TRY(hipStreamWaitEvent(s, u.ev_comm, 0));
+    }
     *cur_out = cur;
     return 0;
 }
 
 }  // namespace
 
-// The distributed heat loop (see dist_run). dtype 0 = f32, 1 = f64.
-// tblock 1: one step per exchange; 2: two steps per exchange (needs 2B-deep
-// halos, `interior` shrunk by 2B on neighbour sides, `ext` = owned region
-// grown by B on neighbour sides). fma: FMA-contracted stencil.
-CME_EXPORT int cme_heat_dist_run(void* comm, void* buf0, void* buf1, int pitch, int gy, const int* interior, int n_int,
-                                 const int* border, int n_b, const int* ext, int tblock, int fma,
-                                 const long long* rows, int n_rows, const int* cols,
-                                 int n_cols, void* stage, int dtype, int order, double xcfl, double ycfl, int iters,
-                                 int cur, int sync, int exchange_first, int* cur_out, void* stream) {
+// The distributed heat loop (see dist_run). transport 0 = RCCL (`comm`, one
+// sub), 1 = loopback (every neighbour is one of `subs`), 2 = none (halos are
+// not exchanged; benchmarks/bench_dist_rank.py). dtype 0 f32, 1 f64.
+// tblock 1: one step per exchange; 2: two steps per exchange (2B-deep halos,
+// `interior` shrunk by 2B on neighbour sides, `ext` = owned region grown by B
+// on neighbour sides). fma: FMA-contracted stencil.
+CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, int nsub, int dtype, int order,
+                                 double xcfl, double ycfl, int iters, int cur, int sync, int exchange_first,
+                                 int tblock, int fma, int* cur_out, void* stream) {
+    const SubDesc* sd = (const SubDesc*)subs;
     if (dtype == 0)
-        return dist_run<float>((ncclComm_t)comm, (float*)buf0, (float*)buf1, pitch, gy, interior, n_int, border, n_b,
-                               ext, tblock, fma, rows, n_rows, cols, n_cols, (float*)stage, order, (float)xcfl, (float)ycfl, iters, cur,
-                               sync, exchange_first, cur_out, as_stream(stream));
-    return dist_run<double>((ncclComm_t)comm, (double*)buf0, (double*)buf1, pitch, gy, interior, n_int, border, n_b,
-                            ext, tblock, fma, rows, n_rows, cols, n_cols, (double*)stage, order, xcfl, ycfl, iters, cur, sync,
-                            exchange_first, cur_out, as_stream(stream));
+        return dist_run<float>(transport, (ncclComm_t)comm, sd, nsub, order, (float)xcfl, (float)ycfl, iters, cur,
+                               sync, exchange_first, tblock, fma, cur_out, as_stream(stream));
+    return dist_run<double>(transport, (ncclComm_t)comm, sd, nsub, order, xcfl, ycfl, iters, cur, sync,
+                            exchange_first, tblock, fma, cur_out, as_stream(stream));
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)

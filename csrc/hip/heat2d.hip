@@ -338,15 +338,29 @@ __device__ __forceinline__ void stream2_run(const T* src, T* dst, int pitch, int
     st.run();
 }
 
+// Up to four output regions per launch (a distributed subdomain's border
+// strips go out as ONE launch); every region shares the step-1 region.
+constexpr int kMaxS2Regions = 4;
+struct S2Regions {
+    int n;
+    int xb[kMaxS2Regions], xe[kMaxS2Regions], yb[kMaxS2Regions], ye[kMaxS2Regions];
+    int strips[kMaxS2Regions], chunk[kMaxS2Regions];
+    int wave_end[kMaxS2Regions];  // cumulative wave counts
+};
+
 template <typename T, int ORDER, int RB, bool FMA, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_stream2_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
-                                                           int gy, int xb, int xe, int yb, int ye, int xb1,
-                                                           int xe1, int yb1, int ye1, int strips, int chunk,
-                                                           int total_waves, T xcfl, T ycfl) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_stream2_kernel(
+    const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
+    int ye1, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
     const int lane = lane_id();
-    const int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
-    if (wave >= total_waves) return;
+    int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
+    if (wave >= R.wave_end[R.n - 1]) return;
+    int r = 0;
+    while (wave >= R.wave_end[r]) ++r;  // wave-uniform, <= 3 steps
+    if (r > 0) wave -= R.wave_end[r - 1];
+    const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
+    const int strips = R.strips[r], chunk = R.chunk[r];
     const int strip = wave % strips;
     const int ck = wave / strips;
     const int y0 = yb + ck * chunk;
@@ -380,29 +394,64 @@ struct Region {
 // Defaults from benchmarks/tune_heat2.py (16384^2, order 8; profiles/
 // heat_stream2_tune.md): rows per block RB and a target wave count that sets
 // the row chunk (more, shorter chunks win for the lighter FMA kernel).
-template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
-int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
-                   hipStream_t s) {
-    const int H = g.ye - g.yb;
-    if (H <= 0 || g.xe <= g.xb) return 0;
-    const int x_lo = g.xb & ~3;
-    const int strips = (int)cdiv(g.xe - x_lo, kStrip2Out);
-    int chunk = chunk_hint;
+template <typename T, bool FMA, int RB>
+int stream2_chunk(int strips, int H, int chunk_hint) {
+    static const int env_chunk = [] {
+        const char* e = getenv("CME_STREAM2_CHUNK");  // tuning experiments only
+        return e ? atoi(e) : 0;
+    }();
+    int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
         const long target_waves = 256L * (sizeof(T) == 4 ? (FMA ? 128 : 48) : 24);
         long rows = ((long)strips * H + target_waves - 1) / target_waves;
         const long lo = 4 * RB > 16 ? 4 * RB : 16;
-        rows = rows < lo ? lo : rows;
+        if ((long)strips * cdiv(H, lo) < 1024) {
+            // thin region (a distributed border strip, on the critical path
+            // after each halo exchange): latency-bound, so trade redundant
+            // halo rows for parallelism -- about 1024 waves, >= RB rows each
+            rows = ((long)strips * H + 1023) / 1024;
+            rows = rows < RB ? RB : rows;
+        } else {
+            rows = rows < lo ? lo : rows;
+        }
         rows = rows > 512 ? 512 : rows;
         chunk = (int)rows;
     }
-    chunk = ((chunk + RB - 1) / RB) * RB;
-    const int chunks = (int)cdiv(H, chunk);
-    const int total_waves = strips * chunks;
-    hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB, FMA, WPE>), dim3(cdiv(total_waves, 4)), dim3(256), 0, s, prev, curr,
-                       pitch, gy, g.xb, g.xe, g.yb, g.ye, g1.xb, g1.xe, g1.yb, g1.ye, strips, chunk, total_waves, xcfl,
-                       ycfl);
+    return ((chunk + RB - 1) / RB) * RB;
+}
+
+// Two-step pass over `n` output regions `gs` (<= 4, one launch); step-1
+// region `g1` must contain them and extend at most B cells beyond.
+template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
+int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl,
+                         T ycfl, int chunk_hint, hipStream_t s) {
+    if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
+    S2Regions R{};
+    int waves = 0;
+    for (int i = 0; i < n; ++i) {
+        const Region& g = gs[i];
+        const int H = g.ye - g.yb;
+        if (H <= 0 || g.xe <= g.xb) continue;  // empty region: no waves
+        const int strips = (int)cdiv(g.xe - (g.xb & ~3), kStrip2Out);
+        const int chunk = stream2_chunk<T, FMA, RB>(strips, H, chunk_hint);
+        const int k = R.n++;
+        R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
+        R.strips[k] = strips;
+        R.chunk[k] = chunk;
+        waves += strips * (int)cdiv(H, chunk);
+        R.wave_end[k] = waves;
+    }
+    if (R.n == 0) return 0;
+    hipLaunchKernelGGL((heat_stream2_kernel<T, ORDER, RB, FMA, WPE>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
+                       curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
     CME_LAUNCH_STATUS();
+}
+
+template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
+int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
+                   hipStream_t s) {
+    return launch_stream2_multi<T, ORDER, FMA, RB, WPE>(prev, curr, pitch, gy, &g, 1, g1, xcfl, ycfl, chunk_hint, s);
 }
 
 namespace {
@@ -472,39 +521,47 @@ int dispatch_heat(int order, int variant, const T* prev, T* curr, int pitch, int
 }
 
 template <typename T, bool FMA>
-int dispatch_stream2_t(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
-                       int chunk, hipStream_t s) {
+int dispatch_stream2_t(int order, const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1,
+                       T xcfl, T ycfl, int chunk, hipStream_t s) {
     switch (order) {
-        case 2: return launch_stream2<T, 2, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
-        case 4: return launch_stream2<T, 4, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
-        case 8: return launch_stream2<T, 8, FMA>(prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+        case 2: return launch_stream2_multi<T, 2, FMA>(prev, curr, pitch, gy, gs, n, g1, xcfl, ycfl, chunk, s);
+        case 4: return launch_stream2_multi<T, 4, FMA>(prev, curr, pitch, gy, gs, n, g1, xcfl, ycfl, chunk, s);
+        case 8: return launch_stream2_multi<T, 8, FMA>(prev, curr, pitch, gy, gs, n, g1, xcfl, ycfl, chunk, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
 
 template <typename T>
-int dispatch_stream2(int order, const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl,
-                     int chunk, int fma, hipStream_t s) {
-    return fma ? dispatch_stream2_t<T, true>(order, prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s)
-               : dispatch_stream2_t<T, false>(order, prev, curr, pitch, gy, g, g1, xcfl, ycfl, chunk, s);
+int dispatch_stream2(int order, const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1,
+                     T xcfl, T ycfl, int chunk, int fma, hipStream_t s) {
+    return fma ? dispatch_stream2_t<T, true>(order, prev, curr, pitch, gy, gs, n, g1, xcfl, ycfl, chunk, s)
+               : dispatch_stream2_t<T, false>(order, prev, curr, pitch, gy, gs, n, g1, xcfl, ycfl, chunk, s);
 }
 
 }  // namespace
 
 // TWO timesteps in one pass: curr[out] = FTCS^2(prev) where the intermediate
 // step is applied on region `ext` (out grown by <= B cells into a halo).
-// fma: 0 exact (contraction off), 1 FMA-contracted stencil.
-CME_EXPORT int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, float xcfl, float ycfl, int chunk, int fma, void* stream) {
-    return dispatch_stream2<float>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
-                                   Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, fma, as_stream(stream));
+// fma: 0 exact (contraction off), 1 FMA-contracted stencil. `out` holds
+// nout (<= 4) regions {xb, xe, yb, ye}, done in ONE launch.
+CME_EXPORT int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, float xcfl, float ycfl, int chunk, int fma,
+                                  void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    return dispatch_stream2<float>(order, prev, curr, pitch, gy, gs, nout, Region{ext[0], ext[1], ext[2], ext[3]},
+                                   xcfl, ycfl, chunk, fma, as_stream(stream));
 }
 
-CME_EXPORT int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, const int* ext,
-                                  int order, double xcfl, double ycfl, int chunk, int fma, void* stream) {
-    return dispatch_stream2<double>(order, prev, curr, pitch, gy, Region{out[0], out[1], out[2], out[3]},
-                                    Region{ext[0], ext[1], ext[2], ext[3]}, xcfl, ycfl, chunk, fma,
-                                    as_stream(stream));
+CME_EXPORT int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, double xcfl, double ycfl, int chunk, int fma,
+                                  void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    return dispatch_stream2<double>(order, prev, curr, pitch, gy, gs, nout, Region{ext[0], ext[1], ext[2], ext[3]},
+                                    xcfl, ycfl, chunk, fma, as_stream(stream));
 }
 
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO

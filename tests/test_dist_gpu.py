@@ -80,6 +80,39 @@ def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype, fma):
     assert np.array_equal(sim.gather_global(), ref.gather_global())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,world", [(1, 4), (2, 4), (2, 6), (1, 3)])
+@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("tblock,fma,dtype", [(1, False, torch.float32), (2, False, torch.float64),
+                                              (2, True, torch.float32)])
+def test_native_loop_loopback_transport(gpu, method, world, sync, tblock, fma, dtype):
+    """The native loop (border stream || interior stream || exchange stream,
+    double-buffered events) with the loopback transport: several subdomains
+    in one process, halos pulled with device copies. Must equal the
+    single-grid CPU oracle bit for bit -- this is the schedule bench.py runs
+    across GPUs with the RCCL transport."""
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=333, ny=270, order=8, iters=7, sync=sync, grid_method=method, ic=5.0,
+                  bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
+    ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)
+    sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=tblock, fma=fma)
+    for d in (ref, sim):
+        for s in d.subs.values():
+            g, b = s.grid, s.blk
+            H = g.H
+            yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+            ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0).to(dtype)
+            g.buf[:, H:H + b.ny, H:H + b.nx] = ic.to(g.device)
+        d.exchange(d._cur()).wait()
+    ref.run(p.iters)
+    sim.run_native(3)
+    sim.run_native(4)  # two calls: state / halos carried across calls
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
+
+
 def _two_ranks_same_gpu(rank, world, method, sync, native):
     import torch
     import torch.distributed as dist
