@@ -13,7 +13,8 @@ from .. import _ext
 _ext.proto(_ext.HIP_PROTOS, "cme_transpose_f32", "ppiiip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_transpose_f32", "ppiii")
 
-VARIANTS = {"copy": 0, "naive": 1, "lds": 2, "lds_pad": 3, "lds_swizzle": 4, "diagonal": 5, "xcd": 6, "vec": 7}
+VARIANTS = {"copy": 0, "naive": 1, "lds": 2, "lds_pad": 3, "lds_swizzle": 4, "diagonal": 5, "xcd": 6, "vec": 7,
+            "vec_xcd": 8}
 
 
 def transpose(x: torch.Tensor, variant: str = "vec", out: torch.Tensor | None = None) -> torch.Tensor:

@@ -21,7 +21,7 @@ def main():
     y = torch.empty_like(x)
     ws = workspace(x.device, (n // 1024 + 1) * 8 + 16)
     s = _ext.stream_ptr()
-    cfgs = [(r, lb) for r in (4, 8) for lb in (1, 0)]
+    cfgs = [(r, lb) for r in (4, 8, 16) for lb in (1, 0)]
     fns = {c: (lambda c=c: _ext.call_hip("cme_scan_tune", x.data_ptr(), y.data_ptr(), n, c[0], c[1],
                                          ws.data_ptr(), s)) for c in cfgs}
     fns["cumsum"] = lambda: torch.cumsum(x, 0, out=y)
@@ -49,5 +49,39 @@ def main():
         print(json.dumps({"rows": r, "max_rel_err": err}))
 
 
+def spmv_main():
+    """--spmv: segmented (SpMV-scan) look-back variants on three final-project
+    shapes: rows per lane 4/8 x next-tile prefetch."""
+    import torch
+
+    import cme213x
+    from cme213x import _ext
+    from cme213x.models.spmv_scan import BENCH_SHAPES, SpmvScanSolver, generate
+    from cme213x.ops.scan import _lookback_ws
+
+    _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_tune", "pppqipiip")
+    s = _ext.stream_ptr()
+    for name in ("pwtk", "webbase-1M", "mac_econ_fwd500"):
+        n, p, N = BENCH_SHAPES[name]
+        sol = SpmvScanSolver(generate(n, p, 100000, N, seed=1), "cuda")
+        ws = _lookback_ws(sol.a)
+        for rows in (4, 8):
+            for pf in (1, 0):
+                f = lambda: _ext.call_hip("cme_spmv_scan_tune", sol.a.data_ptr(), sol.xx.data_ptr(),  # noqa
+                                          sol.flags.data_ptr(), n, N, ws.data_ptr(), rows, pf, s)
+                f()
+                ts = []
+                for _ in range(5):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    f()
+                    e1.record()
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                ms = sorted(ts)[2]
+                print(json.dumps({"matrix": name, "rows": rows, "prefetch": pf, "ms": round(ms, 4),
+                                  "GBps": round(12 * n * N / ms / 1e6)}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    spmv_main() if "--spmv" in sys.argv else main()

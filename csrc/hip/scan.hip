@@ -26,6 +26,10 @@ constexpr int kScanThreads = 256;
 constexpr int kScanWaves = kScanThreads / kWave;
 constexpr int kScanItemsPerLane = 16;  // 4 x 16-B vectors
 constexpr int kScanTile = kScanThreads * kScanItemsPerLane;  // 4096
+// rows of 16-B vectors per lane in the production look-back scan: 8 (8192-
+// element tiles) halves the number of sequential look-back rounds vs 4;
+// benchmarks/tune_scan.py at 2^26: 0.138 ms (8) vs 0.170 (4) vs 0.142 (16)
+constexpr int kLbRows = 8;
 
 template <typename T>
 struct Vec4 {
@@ -82,13 +86,18 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     // at most 4 blocks of 256 per CU: co-resident), so every tile's
     // predecessors are owned by running blocks -- no ordering ticket (a single
     // atomic word saturates at ~88 ops/us) and no dispatch-order assumption.
-    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
+    // The next tile's loads are issued before this tile's look-back wait, so
+    // two tiles of loads are in flight per block (the scan is latency-bound
+    // on the look-back hand-off, not on bandwidth).
     const int wid = threadIdx.x / kWave;
-    const long long base = (long long)tile * TILE + wid * WAVE_ELEMS;
-
     Vec4<T> v[ROWS];
+    if (blockIdx.x < tiles) {
+        const long long b0 = (long long)blockIdx.x * TILE + wid * WAVE_ELEMS;
 #pragma unroll
-    for (int k = 0; k < ROWS; ++k) v[k] = load_v4(in, base + k * 256 + lane * 4, n, T(0));
+        for (int k = 0; k < ROWS; ++k) v[k] = load_v4(in, b0 + k * 256 + lane * 4, n, T(0));
+    }
+    for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
+    const long long base = (long long)tile * TILE + wid * WAVE_ELEMS;
 
     // in-lane inclusive scan of each 4-vector, wave scans of the lane totals,
     // serial carry across the wave-rows
@@ -121,6 +130,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
         if (w < wid) wpre = wpre + t;
         tot = tot + t;
     }
+    if (LOOKBACK && wid == 0 && lane == 0 && tile > 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
+    // prefetch the next tile of this block while the look-back resolves
+    Vec4<T> vn[ROWS];
+    const int next = tile + gridDim.x;
+    if (next < tiles) {
+        const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
+    }
     if (!LOOKBACK) {
         if (threadIdx.x == 0) s_prefix[parity] = T(0);
     } else if (wid == 0) {
@@ -130,7 +148,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
                 s_prefix[parity] = T(0);
             }
         } else {
-            if (lane == 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
             T pre = lb_lookback<T, false>(desc, tile, timeout);
             if (lane == 0) {
                 lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
@@ -146,6 +163,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
         Vec4<T> r{q + v[k].x, q + v[k].y, q + v[k].z, q + v[k].w};
         store_v4(out, base + k * 256 + lane * 4, n, r);
     }
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) v[k] = vn[k];
     }  // tile loop
 }
 
@@ -419,59 +438,91 @@ __device__ __forceinline__ float wave_segscan(float v, uint32_t f, uint32_t* f_o
 
 // flags source: MODE 0 = uint8 per element, MODE 1 = bitmask words (bit i%32
 // of word i/32). FUSED_MUL: v = a[i]*x[i] before scanning (final project).
+// Raw per-row inputs of one lane (loads only; decoding and the fused
+// multiply happen at use, so a prefetch never waits on memory).
+struct SegRaw {
+    Vec4<float> a, x;
+    uint32_t fw;  // MODE 0: 4 flag bytes; MODE 1: the bitmask word
+};
+
 template <int MODE, bool FUSED_MUL>
+__device__ __forceinline__ SegRaw seg_load(const float* __restrict__ in, const float* __restrict__ xmul,
+                                           const void* __restrict__ flags, long long i, long long n) {
+    SegRaw r;
+    r.a = load_v4(in, i, n, 0.f);
+    if constexpr (FUSED_MUL) r.x = load_v4(xmul, i, n, 0.f);
+    if constexpr (MODE == 0) {
+        const uint8_t* fp = (const uint8_t*)flags;
+        if (i + 3 < n) {
+            r.fw = *reinterpret_cast<const uint32_t*>(fp + i);
+        } else {
+            r.fw = 0;
+            for (int j = 0; j < 4; ++j)
+                if (i + j < n && fp[i + j]) r.fw |= 1u << (8 * j);
+        }
+    } else {
+        const uint32_t* fw = (const uint32_t*)flags;
+        r.fw = i < n ? fw[i >> 5] : 0u;
+    }
+    return r;
+}
+
+// ROWS 16-B vectors per lane per tile; PREFETCH issues the next tile's loads
+// before the look-back wait (two tiles of loads in flight per block).
+// Production: ROWS 4, no prefetch (benchmarks/tune_scan.py --spmv: prefetch
+// and 8 rows both lose to register pressure -- profiles/spmv_scan_tune.jsonl).
+template <int MODE, bool FUSED_MUL, int ROWS = 4, bool PREFETCH = false>
 __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
                                                                float* __restrict__ out, const void* __restrict__ flags,
                                                                long long n, uint64_t* desc, int tiles,
                                                                unsigned* timeout, uint32_t epoch) {
+    constexpr int TILE = kScanThreads * 4 * ROWS;
+    constexpr int WAVE_ELEMS = kWave * 4 * ROWS;
     __shared__ float s_wv_[2][kScanWaves];
     __shared__ uint32_t s_wf_[2][kScanWaves];
     __shared__ float s_prefix_[2];
     const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
     int parity = 0;
+    SegRaw raw[ROWS];
+    if (blockIdx.x < tiles) {
+        const long long b0 = (long long)blockIdx.x * TILE + wid * WAVE_ELEMS;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, b0 + k * 256 + lane * 4, n);
+    }
     // persistent, co-resident grid (see scan_lookback_kernel)
     for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
     float* s_wv = s_wv_[parity];
     uint32_t* s_wf = s_wf_[parity];
     float& s_prefix = s_prefix_[parity];
-    const int wid = threadIdx.x / kWave;
-    const long long base = (long long)tile * kScanTile + wid * (kWave * 16);
+    const long long base = (long long)tile * TILE + wid * WAVE_ELEMS;
 
-    float val[4][4];
-    uint32_t fl[4][4];
-    float run_v = 0.f;   // running (segment-aware) value across the 4 rows
+    float val[ROWS][4];
+    uint32_t flm[ROWS];  // bit j: a head at or before element j of the lane's 4
+    float run_v = 0.f;   // running (segment-aware) value across the rows
     uint32_t run_f = 0;  // any head seen so far in this wave
-    float ex_v[4];
-    uint32_t ex_f[4];
+    float ex_v[ROWS];
+    uint32_t ex_f[ROWS];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < ROWS; ++k) {
         const long long i = base + k * 256 + lane * 4;
-        Vec4<float> a = load_v4(in, i, n, 0.f);
+        Vec4<float> a = raw[k].a;
         if constexpr (FUSED_MUL) {
-            Vec4<float> x = load_v4(xmul, i, n, 0.f);
-            a.x *= x.x;
-            a.y *= x.y;
-            a.z *= x.z;
-            a.w *= x.w;
+            a.x *= raw[k].x.x;
+            a.y *= raw[k].x.y;
+            a.z *= raw[k].x.z;
+            a.w *= raw[k].x.w;
         }
         uint32_t f4;
         if constexpr (MODE == 0) {
-            const uint8_t* fp = (const uint8_t*)flags;
-            if (i + 3 < n) {
-                f4 = *reinterpret_cast<const uint32_t*>(fp + i);
-                f4 = (f4 & 1u) | ((f4 >> 7) & 2u) | ((f4 >> 14) & 4u) | ((f4 >> 21) & 8u);
-            } else {
-                f4 = 0;
-                for (int j = 0; j < 4; ++j)
-                    if (i + j < n && fp[i + j]) f4 |= 1u << j;
-            }
+            const uint32_t w = raw[k].fw;
+            f4 = (w & 1u) | ((w >> 7) & 2u) | ((w >> 14) & 4u) | ((w >> 21) & 8u);
         } else {
-            const uint32_t* fw = (const uint32_t*)flags;
-            f4 = i < n ? (fw[i >> 5] >> (i & 31)) & 0xfu : 0u;
+            f4 = (raw[k].fw >> (i & 31)) & 0xfu;
         }
         // in-lane inclusive segmented scan of 4 values
         float v0 = a.x, v1 = a.y, v2 = a.z, v3 = a.w;
-        uint32_t g0 = f4 & 1, g1 = (f4 >> 1) & 1, g2 = (f4 >> 2) & 1, g3 = (f4 >> 3) & 1;
+        const uint32_t g0 = f4 & 1, g1 = (f4 >> 1) & 1, g2 = (f4 >> 2) & 1, g3 = (f4 >> 3) & 1;
         v1 = g1 ? v1 : v0 + v1;
         v2 = g2 ? v2 : v1 + v2;
         v3 = g3 ? v3 : v2 + v3;
@@ -479,13 +530,11 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
         val[k][1] = v1;
         val[k][2] = v2;
         val[k][3] = v3;
-        fl[k][0] = g0;
-        fl[k][1] = g0 | g1;
-        fl[k][2] = g0 | g1 | g2;
-        fl[k][3] = g0 | g1 | g2 | g3;
+        const uint32_t c1 = g0 | g1, c2 = c1 | g2, c3 = c2 | g3;
+        flm[k] = g0 | (c1 << 1) | (c2 << 2) | (c3 << 3);
         // wave scan of lane totals (value v3, flag = any head in lane)
         uint32_t lf;
-        float inc = wave_segscan(v3, fl[k][3], &lf);
+        float inc = wave_segscan(v3, c3, &lf);
         // exclusive (shift by one lane); lane 0 gets the carry from earlier rows
         float e_v = dpp_move<kDppWaveShr1>(0.f, inc);
         uint32_t e_f = dpp_move<kDppWaveShr1>(0u, lf);
@@ -519,15 +568,22 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
         tot_v = tf ? tv : tot_v + tv;
         tot_f |= tf;
     }
+    const uint32_t hf = tot_f ? kStFlag : 0u;
+    if (wid == 0 && lane == 0 && tile > 0)
+        lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
+    const int next = tile + gridDim.x;
+    if (PREFETCH && next < tiles) {
+        const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, nb + k * 256 + lane * 4, n);
+    }
     if (wid == 0) {
-        const uint32_t hf = tot_f ? kStFlag : 0u;
         if (tile == 0) {
             if (lane == 0) {
                 lb_publish(desc, kStInclusive | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
                 s_prefix = 0.f;
             }
         } else {
-            if (lane == 0) lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
             float pre = lb_lookback<float, true>(desc, tile, timeout, epoch);
             if (lane == 0) {
                 float incl = tot_f ? tot_v : pre + tot_v;
@@ -541,14 +597,19 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     const float tile_pre = s_prefix;
     const float wcarry = wpre_f ? wpre_v : tile_pre + wpre_v;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < ROWS; ++k) {
         const float c = ex_f[k] ? ex_v[k] : wcarry + ex_v[k];
         Vec4<float> r;
-        r.x = fl[k][0] ? val[k][0] : c + val[k][0];
-        r.y = fl[k][1] ? val[k][1] : c + val[k][1];
-        r.z = fl[k][2] ? val[k][2] : c + val[k][2];
-        r.w = fl[k][3] ? val[k][3] : c + val[k][3];
+        r.x = (flm[k] & 1u) ? val[k][0] : c + val[k][0];
+        r.y = (flm[k] & 2u) ? val[k][1] : c + val[k][1];
+        r.z = (flm[k] & 4u) ? val[k][2] : c + val[k][2];
+        r.w = (flm[k] & 8u) ? val[k][3] : c + val[k][3];
         store_v4(out, base + k * 256 + lane * 4, n, r);
+    }
+    if (!PREFETCH && next < tiles) {
+        const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, nb + k * 256 + lane * 4, n);
     }
     }  // tile loop
 }
@@ -556,19 +617,19 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
 template <typename T>
 int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
-    const int tiles = (int)((n + kScanTile - 1) / kScanTile);
-    static int bpc_e = persistent_blocks_per_cu(scan_lookback_kernel<T, true, kScanItemsPerLane / 4>, kScanThreads);
-    static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kScanItemsPerLane / 4>, kScanThreads);
+    const int tiles = (int)((n + 1024LL * kLbRows - 1) / (1024LL * kLbRows));
+    static int bpc_e = persistent_blocks_per_cu(scan_lookback_kernel<T, true, kLbRows>, kScanThreads);
+    static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows>, kScanThreads);
     const int cap = kNumCU * (exclusive ? bpc_e : bpc_i);
     const int grid = tiles < cap ? tiles : cap;
     uint64_t* desc = (uint64_t*)ws;
     unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
     if (exclusive)
-        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kScanItemsPerLane / 4>), dim3(grid), dim3(kScanThreads), 0,
+        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows>), dim3(grid), dim3(kScanThreads), 0,
                            s, in, out, n, desc, tiles, timeout);
     else
-        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kScanItemsPerLane / 4>), dim3(grid), dim3(kScanThreads), 0,
+        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows>), dim3(grid), dim3(kScanThreads), 0,
                            s, in, out, n, desc, tiles, timeout);
     CME_LAUNCH_STATUS();
 }
@@ -736,24 +797,44 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
 
 // Final-project driver: `iters` fused steps a <- segscan(a * xx) (bitmask
 // heads) with ONE descriptor memset; iteration i uses look-back epoch i+1.
-CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
-                                 void* stream) {
-    hipStream_t s = as_stream(stream);
-    if (n <= 0 || iters <= 0) return 0;
-    const int tiles = (int)((n + kScanTile - 1) / kScanTile);
-    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
+namespace {
+template <int ROWS, bool PF>
+int spmv_scan_launch(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
+                     hipStream_t s) {
+    constexpr long long TILE = 1024LL * ROWS;
+    const int tiles = (int)((n + TILE - 1) / TILE);
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF>, kScanThreads);
     const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
     uint64_t* desc = (uint64_t*)ws;
     unsigned* timeout = (unsigned*)(desc + tiles);
     CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
     for (int it = 0; it < iters; ++it)
-        hipLaunchKernelGGL((segscan_kernel<1, true>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a, flags, n, desc,
-                           tiles, timeout, (uint32_t)(it + 1));
+        hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a, flags,
+                           n, desc, tiles, timeout, (uint32_t)(it + 1));
     CME_LAUNCH_STATUS();
+}
+}  // namespace
+
+CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
+                                 void* stream) {
+    if (n <= 0 || iters <= 0) return 0;
+    return spmv_scan_launch<4, false>(a, xx, flags, n, iters, ws, as_stream(stream));
+}
+
+// Tuning entry (benchmarks/tune_scan.py --spmv): rows 4/8 x prefetch on/off.
+CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
+                                  int rows, int prefetch, void* stream) {
+    if (n <= 0 || iters <= 0) return 0;
+    hipStream_t s = as_stream(stream);
+    if (rows == 4) return prefetch ? spmv_scan_launch<4, true>(a, xx, flags, n, iters, ws, s)
+                                   : spmv_scan_launch<4, false>(a, xx, flags, n, iters, ws, s);
+    if (rows == 8) return prefetch ? spmv_scan_launch<8, true>(a, xx, flags, n, iters, ws, s)
+                                   : spmv_scan_launch<8, false>(a, xx, flags, n, iters, ws, s);
+    return (int)hipErrorInvalidValue;
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kScanItemsPerLane / 4>);
+CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kLbRows>);
 CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
 CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
 CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true>);

@@ -13,9 +13,10 @@
 //  5 diagonal    : lds_pad with the paper's diagonal block reordering
 //                  (partition camping); on MI355X the analogous lever is
 //  6 xcd         : lds_pad with the bijective XCD-aware block remap
-//  7 vec         : 64x64 tile, 16-B global loads AND stores, pad-65 LDS
-//                  (2-way conflicts on the scalar LDS side, 4x fewer global
-//                  instructions) -- the production variant
+//  7 vec         : 16-B global loads AND stores, pad-(TR+1) LDS, tile shape
+//                  and block order from a measured sweep (vec_tile_kernel)
+//                  -- the production variant
+//  8 vec_xcd     : 64x64 vector tile in XCD-aware block order
 #include "cme213/common.h"
 
 namespace {
@@ -72,42 +73,94 @@ __global__ __launch_bounds__(256) void tile_kernel(const float* __restrict__ in,
     }
 }
 
-// 16-B global accesses on both sides. Requires rows % 4 == 0 && cols % 4 == 0.
-__global__ __launch_bounds__(256) void vec_kernel(const float* __restrict__ in, float* __restrict__ out, int rows,
-                                                  int cols) {
-    constexpr int P = kT + 1;
-    __shared__ float tile[kT * P];
+// Generalised vector tile: TR input rows x TC input columns per 256-thread
+// block (16-B global loads and stores; the transposed tile lives in LDS with
+// a +1 pitch). Taller tiles give longer contiguous output-row segments
+// (TR floats), wider tiles longer input-row segments (TC floats) -- at 8192^2
+// (beyond the 256 MB MALL) 256-B segments at a 32 KB stride leave HBM
+// bandwidth on the table. REMAP: 0 none, 1 XCD-aware, 2 diagonal.
+template <int TR, int TC, int REMAP>
+__global__ __launch_bounds__(256) void vec_tile_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                       int rows, int cols) {
+    constexpr int P = TR + 1;
+    __shared__ float tile[TC * P];
     const int t = threadIdx.x;
-    const unsigned lin = blockIdx.y * gridDim.x + blockIdx.x;
-    const unsigned r = xcd_remap(lin, gridDim.x * gridDim.y);
-    const int bx = r % gridDim.x, by = r / gridDim.x;
-    const int x0 = bx * kT, y0 = by * kT;
-    const int c4 = (t % 16) * 4;
+    int bx = blockIdx.x, by = blockIdx.y;
+    if constexpr (REMAP == 1) {
+        const unsigned lin = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned r = xcd_remap(lin, gridDim.x * gridDim.y);
+        bx = r % gridDim.x;
+        by = r / gridDim.x;
+    } else if constexpr (REMAP == 2) {
+        if (gridDim.x == gridDim.y) {
+            by = blockIdx.x;
+            bx = (blockIdx.x + blockIdx.y) % gridDim.x;
+        }
+    }
+    const int x0 = bx * TC, y0 = by * TR;
+    constexpr int LPR = TC / 4;              // lanes per input row
+    constexpr int RPP = 256 / LPR;           // rows per pass
+    const int c4 = (t % LPR) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int rr = t / 16 + 16 * i;
+    for (int i = 0; i < TR / RPP; ++i) {
+        const int rr = t / LPR + RPP * i;
         const int y = y0 + rr, x = x0 + c4;
         if (y < rows && x < cols) {
             const float4 v = *reinterpret_cast<const float4*>(in + (size_t)y * cols + x);
-            tile[(c4 + 0) * P + rr] = v.x;  // store transposed: tile[col][row]
+            tile[(c4 + 0) * P + rr] = v.x;
             tile[(c4 + 1) * P + rr] = v.y;
             tile[(c4 + 2) * P + rr] = v.z;
             tile[(c4 + 3) * P + rr] = v.w;
         }
     }
     __syncthreads();
+    constexpr int LPO = TR / 4;              // lanes per output row
+    constexpr int OPP = 256 / LPO;           // output rows per pass
+    const int r4 = (t % LPO) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int oc = t / 16 + 16 * i;  // output row within tile (= input column)
-        const int oy = x0 + oc, ox = y0 + c4;
+    for (int i = 0; i < TC / OPP; ++i) {
+        const int oc = t / LPO + OPP * i;
+        const int oy = x0 + oc, ox = y0 + r4;
         if (oy < cols && ox < rows) {
-            const float* s = &tile[oc * P + c4];
+            const float* s = &tile[oc * P + r4];
             *reinterpret_cast<float4*>(out + (size_t)oy * rows + ox) = make_float4(s[0], s[1], s[2], s[3]);
         }
     }
 }
 
+template <int TR, int TC, int REMAP>
+int launch_vec_tile(const float* in, float* out, int rows, int cols, hipStream_t s) {
+    dim3 grid(cdiv(cols, TC), cdiv(rows, TR));
+    hipLaunchKernelGGL((vec_tile_kernel<TR, TC, REMAP>), grid, dim3(256), 0, s, in, out, rows, cols);
+    CME_LAUNCH_STATUS();
+}
+
 }  // namespace
+
+// Tuning sweep entry (benchmarks/tune_transpose.py): tile rows tr in
+// {64, 128, 256}, tile cols tc in {64, 128}, remap 0/1/2.
+CME_EXPORT int cme_transpose_tune(const float* in, float* out, int rows, int cols, int tr, int tc, int remap,
+                                  void* stream) {
+    hipStream_t s = as_stream(stream);
+    if ((rows % 4) || (cols % 4)) return (int)hipErrorInvalidValue;
+#define CME_VT(TR, TC)                                                                 \
+    if (tr == TR && tc == TC) {                                                        \
+        switch (remap) {                                                               \
+            case 0: return launch_vec_tile<TR, TC, 0>(in, out, rows, cols, s);         \
+            case 1: return launch_vec_tile<TR, TC, 1>(in, out, rows, cols, s);         \
+            case 2: return launch_vec_tile<TR, TC, 2>(in, out, rows, cols, s);         \
+            default: return (int)hipErrorInvalidValue;                                 \
+        }                                                                              \
+    }
+    CME_VT(64, 64)
+    CME_VT(128, 64)
+    CME_VT(256, 64)
+    CME_VT(64, 128)
+    CME_VT(128, 128)
+    CME_VT(256, 128)
+#undef CME_VT
+    return (int)hipErrorInvalidValue;
+}
 
 CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols, int variant, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -121,10 +174,18 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
         case 5: hipLaunchKernelGGL((tile_kernel<1, 1>), grid, dim3(256), 0, s, in, out, rows, cols); break;
         case 6: hipLaunchKernelGGL((tile_kernel<1, 2>), grid, dim3(256), 0, s, in, out, rows, cols); break;
         case 7:
-            if ((rows % 4) || (cols % 4) || ((uintptr_t)in % 16) || ((uintptr_t)out % 16))
+        case 8:
+            if ((rows % 4) || (cols % 4) || ((uintptr_t)in % 16) || ((uintptr_t)out % 16)) {
                 hipLaunchKernelGGL((tile_kernel<1, 2>), grid, dim3(256), 0, s, in, out, rows, cols);
-            else
-                hipLaunchKernelGGL(vec_kernel, grid, dim3(256), 0, s, in, out, rows, cols);
+            } else if (variant == 8) {
+                return launch_vec_tile<64, 64, 1>(in, out, rows, cols, s);
+            } else {
+                // benchmarks/tune_transpose.py (profiles/transpose_tune.md):
+                // square -> 64x64 tiles in diagonal order (5.3 TB/s at
+                // 8192^2); otherwise 64x128 tiles (5.3 TB/s at 16384^2)
+                if (rows == cols) return launch_vec_tile<64, 64, 2>(in, out, rows, cols, s);
+                return launch_vec_tile<64, 128, 0>(in, out, rows, cols, s);
+            }
             break;
         default: return (int)hipErrorInvalidValue;
     }
@@ -134,4 +195,4 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(transpose_naive, 256, naive_kernel);
 CME_REGISTER_KERNEL(transpose_lds_pad, 256, tile_kernel<1, 0>);
-CME_REGISTER_KERNEL(transpose_vec, 256, vec_kernel);
+CME_REGISTER_KERNEL(transpose_vec, 256, vec_tile_kernel<64, 64, 2>);
