@@ -32,15 +32,21 @@ def fp_main(argv=None) -> int:
 
 
 def checker_main(argv=None) -> int:
-    from ..models.spmv_scan import errors, load, reference_solution
+    """``checker a.txt x.txt b.txt [--legacy]``: the instructor checker
+    (reference_spMVscan-released.cu); ``--legacy`` uses the older O(len^2)
+    serial algorithm of aux/CheckOutput/serialMV.cu (small inputs)."""
+    from ..models.spmv_scan import errors, load, reference_solution, reference_solution_quadratic
 
-    argv = sys.argv[1:] if argv is None else argv
+    argv = list(sys.argv[1:] if argv is None else argv)
+    legacy = "--legacy" in argv
+    argv = [a for a in argv if a != "--legacy"]
     if len(argv) != 3:
-        print("usage: checker a.txt x.txt b.txt")
+        print("usage: checker a.txt x.txt b.txt [--legacy]")
         return 1
     prob = load(argv[0], argv[1])
     b = np.fromfile(argv[2], sep=" ")
-    e = errors(reference_solution(prob), b[:prob.n])
+    ref = reference_solution_quadratic(prob) if legacy else reference_solution(prob)
+    e = errors(ref, b[:prob.n])
     print(f"Absolute L2 error: {e['L2']:g}\nRelative L2 error: {e['relL2']:g}\n"
           f"Absolute Linf error: {e['Linf']:g}\nRelative Linf error: {e['relLinf']:g}")
     return 0

@@ -67,6 +67,25 @@ def run_hw1_cipher(path: str, replicate: int = 16, shift: int | None = None, dev
             ok = False
             print(f"{name}: first mismatch at {bad[0]}: {gpu[bad[0]]} != {ref_np[bad[0]]}")
         res["variants"][name] = {"ms": t.ms, "GBps_rw": 2 * data.size / t.ms / 1e6, "ok": not bad.size}
+    # library baseline: the solution's thrust::transform(in, constant_iterator
+    # (shift), plus<uchar>) (hw/hw1/solution/cipher_solution.cu:234-245) -> a
+    # framework elementwise op (torch's uint8 add wraps mod 256 like uchar)
+    d_out = torch.add(d_in, shift)
+    t = EventTimer("gpu shift cypher library (torch.add)", device=dev)
+    with t:
+        torch.add(d_in, shift, out=d_out)
+    lib = d_out.cpu().numpy()
+    lib_ok = bool(np.array_equal(lib, ref_np))
+    ok = ok and lib_ok
+    res["variants"]["library"] = {"ms": t.ms, "GBps_rw": 2 * data.size / t.ms / 1e6, "ok": lib_ok}
+    # device -> host of the result (reference PA1 section 1c reports both directions)
+    pinned_out = torch.empty_like(pinned).pin_memory()
+    t = EventTimer("copy from gpu", device=dev)
+    with t:
+        pinned_out.copy_(d_out, non_blocking=True)
+    res["d2h_ms"] = t.ms
+    res["h2d_GBps"] = data.size / res["h2d_ms"] / 1e6
+    res["d2h_GBps"] = data.size / res["d2h_ms"] / 1e6
     if ok:
         print("All CUDA Versions matched reference output.  Outputting ciphered text.")
         ref_np[:orig_len].tofile(out_path)

@@ -173,6 +173,26 @@ def reference_solution(prob: SpmvScanProblem, iters: int | None = None) -> np.nd
     return a
 
 
+def reference_solution_quadratic(prob: SpmvScanProblem, iters: int | None = None) -> np.ndarray:
+    """The OLDER checker's algorithm (``aux/CheckOutput/serialMV.cu:27-37``):
+    every output element re-sums its segment prefix from the segment start,
+    O(len^2) per segment, in double. Same result as :func:`reference_solution`
+    up to summation order; only for small inputs (the CheckOutput fixture)."""
+    a = prob.a.astype(np.float64)
+    xx = prob.x.astype(np.float64)[prob.k]
+    s = prob.s.astype(np.int64)
+    for _ in range(prob.iters if iters is None else iters):
+        b = np.empty_like(a)
+        for lo, hi in zip(s[:-1], s[1:]):
+            for j in range(lo, hi):
+                acc = 0.0
+                for l in range(lo, j + 1):
+                    acc += a[l] * xx[l]
+                b[j] = acc
+        a = b
+    return a
+
+
 def errors(ref: np.ndarray, b: np.ndarray) -> dict:
     """The checker's metrics (``reference_spMVscan-released.cu:64-144``)."""
     ref = ref.astype(np.float64)

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from cme213x.models.spmv_scan import (SpmvScanProblem, SpmvScanSolver, errors, generate, load,
-                                      reference_solution, run_fp, save)
+                                      reference_solution, reference_solution_quadratic, run_fp, save)
 from cme213x.ops.scan import head_flags_from_offsets, reduce, scan, segmented_scan
 
 SMALL = "/root/reference/hw/hw_final/programming/aux/CheckOutput"
@@ -66,6 +66,13 @@ def test_small_fixture_matches_reference_output():
     sol = SpmvScanSolver(prob, "cpu")
     out = sol.run().numpy()
     np.testing.assert_allclose(out, b_ref, rtol=1e-6)
+    # the older checker's O(len^2) algorithm agrees (aux/CheckOutput/serialMV.cu)
+    np.testing.assert_allclose(reference_solution_quadratic(prob), ref, rtol=1e-12)
+
+
+def test_quadratic_checker_matches_vectorised():
+    prob = generate(600, 40, 50, 3, seed=9)
+    np.testing.assert_allclose(reference_solution_quadratic(prob), reference_solution(prob), rtol=1e-9, atol=1e-9)
 
 
 def test_generator_and_io_roundtrip(tmp_path):
