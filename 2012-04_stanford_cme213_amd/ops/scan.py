@@ -21,6 +21,7 @@ from .. import _ext
 _ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_rts", "ppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_mlevel", "ppqiiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_scan_tree", "ppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_reduce", "pqiiippp")
 _ext.proto(_ext.HIP_PROTOS, "cme_segscan", "ppppiqpp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_run", "pppqipp")
@@ -54,8 +55,10 @@ def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
 def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
          algo: str = "rts") -> torch.Tensor:
     """Prefix sum of a 1-D contiguous float32/int32/uint32 tensor.
-    algo: "lookback" (single pass), "rts" (reduce-then-scan, deterministic),
-    "blelloch" or "hillis" (multi-level scan-then-add)."""
+    algo: "lookback" (single pass), "rts" (reduce-then-scan with DPP wave
+    scans, deterministic), "blelloch" / "hillis" (reduce-then-scan whose block
+    level is the lecture's LDS tree algorithm), "blelloch_mlevel" /
+    "hillis_mlevel" (the recursive scan-then-add of my-refs/scan.pdf Fig. 5)."""
     if not x.is_contiguous():
         x = x.contiguous()
     out = torch.empty_like(x) if out is None else out
@@ -68,7 +71,11 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
         elif algo == "rts":
             _ext.call_hip("cme_scan_rts", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           workspace(x.device, 8192, "rts").data_ptr(), s)
-        else:
+        elif algo in ("blelloch", "hillis"):
+            _ext.call_hip("cme_scan_tree", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype],
+                          0 if algo == "blelloch" else 1, int(exclusive), workspace(x.device, 8192, "rts").data_ptr(),
+                          s)
+        elif algo in ("blelloch_mlevel", "hillis_mlevel"):
             if out.data_ptr() == x.data_ptr() and not exclusive:
                 raise ValueError("in-place inclusive multi-level scan is not supported")
             levels, b = 0, (n + 511) // 512
@@ -77,7 +84,9 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
                 b = (b + 511) // 512
             ws = workspace(x.device, (levels + 1) * 4, "mlevel")
             _ext.call_hip("cme_scan_mlevel", x.data_ptr(), out.data_ptr(), n, _DT[x.dtype],
-                          0 if algo == "blelloch" else 1, int(exclusive), ws.data_ptr(), s)
+                          0 if algo == "blelloch_mlevel" else 1, int(exclusive), ws.data_ptr(), s)
+        else:
+            raise ValueError(f"unknown scan algo {algo!r}")
     else:
         _ext.call_cpu("cme_cpu_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive))
     return out

@@ -65,7 +65,7 @@ def main():
         n = 1 << 26
         x = torch.rand(n, device=dev)
         y = torch.empty_like(x)
-        for algo in ("lookback", "blelloch", "hillis"):
+        for algo in ("lookback", "rts", "blelloch", "hillis", "blelloch_mlevel", "hillis_mlevel"):
             ms = timeit(lambda: sc.scan(x, True, y, algo))
             emit(bench="scan", algo=algo, n=n, ms=ms, GBps=8 * n / ms / 1e6, ref_ms=15.85,
                  speedup_vs_ref=15.85 / ms)

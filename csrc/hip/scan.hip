@@ -369,6 +369,125 @@ __global__ void to_inclusive_kernel(const T* __restrict__ in, T* __restrict__ ou
     if (i < n) out[i] += in[i];
 }
 
+// ------------------------------------------------------------ tree scans, rts
+// The lecture's block algorithms (Blelloch work-efficient up/down-sweep,
+// Hillis-Steele) as the block level of a reduce-then-scan (K1/K2 shared with
+// the DPP version above): each thread scans 16 consecutive elements in
+// registers, the 256 thread totals are scanned in LDS by the tree algorithm
+// (conflict-free padding cf()), the chunk carry rides in a register. 12 B per
+// element like rts, instead of the multi-level scheme's 16.
+constexpr int kTreeItems = 16;
+constexpr int kTreeTile = 256 * kTreeItems;
+
+template <typename T, int ALGO>
+__device__ __forceinline__ T tree_block_exclusive(T v, T* s, T* s2, T& total) {
+    const int t = threadIdx.x;
+    if constexpr (ALGO == 0) {  // Blelloch over 256 values
+        s[cf(t)] = v;
+        int offset = 1;
+        for (int d = 128; d > 0; d >>= 1) {
+            __syncthreads();
+            if (t < d) {
+                const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+                s[cf(bi)] += s[cf(ai)];
+            }
+            offset <<= 1;
+        }
+        __syncthreads();
+        total = s[cf(255)];
+        __syncthreads();
+        if (t == 0) s[cf(255)] = T(0);
+        for (int d = 1; d < 256; d <<= 1) {
+            offset >>= 1;
+            __syncthreads();
+            if (t < d) {
+                const int ai = offset * (2 * t + 1) - 1, bi = offset * (2 * t + 2) - 1;
+                const T x = s[cf(ai)];
+                s[cf(ai)] = s[cf(bi)];
+                s[cf(bi)] += x;
+            }
+        }
+        __syncthreads();
+        const T r = s[cf(t)];
+        __syncthreads();
+        return r;
+    } else {  // Hillis-Steele (double-buffered) over 256 values
+        T* src = s;
+        T* dst = s2;
+        src[t] = v;
+        for (int off = 1; off < 256; off <<= 1) {
+            __syncthreads();
+            dst[t] = t >= off ? src[t] + src[t - off] : src[t];
+            T* tmp = src;
+            src = dst;
+            dst = tmp;
+        }
+        __syncthreads();
+        total = src[255];
+        const T r = t ? src[t - 1] : T(0);
+        __syncthreads();
+        return r;
+    }
+}
+
+template <typename T, bool EXCLUSIVE, int ALGO>
+__global__ __launch_bounds__(256) void rts_tree_scan_kernel(const T* __restrict__ in, T* __restrict__ out, long long n,
+                                                            long long chunk, const T* __restrict__ part) {
+    __shared__ T s[cf(256) + 1];
+    __shared__ T s2[ALGO == 1 ? 256 : 1];
+    const long long b0 = (long long)blockIdx.x * chunk;
+    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    T carry = part[blockIdx.x];
+    for (long long t0 = b0; t0 < b1; t0 += kTreeTile) {
+        const long long i0 = t0 + (long long)threadIdx.x * kTreeItems;
+        T v[kTreeItems];
+#pragma unroll
+        for (int k = 0; k < kTreeItems / 4; ++k) {
+            const Vec4<T> q = load_v4(in, i0 + 4 * k, b1, T(0));
+            v[4 * k] = q.x;
+            v[4 * k + 1] = q.y;
+            v[4 * k + 2] = q.z;
+            v[4 * k + 3] = q.w;
+        }
+        T acc = T(0);
+#pragma unroll
+        for (int k = 0; k < kTreeItems; ++k) {  // serial in-thread scan
+            const T x = v[k];
+            v[k] = EXCLUSIVE ? acc : acc + x;
+            acc = acc + x;
+        }
+        T tot;
+        const T pre = carry + tree_block_exclusive<T, ALGO>(acc, s, s2, tot);
+#pragma unroll
+        for (int k = 0; k < kTreeItems / 4; ++k) {
+            Vec4<T> r{pre + v[4 * k], pre + v[4 * k + 1], pre + v[4 * k + 2], pre + v[4 * k + 3]};
+            store_v4(out, i0 + 4 * k, b1, r);
+        }
+        carry = carry + tot;
+    }
+}
+
+template <typename T>
+int launch_tree_rts(const T* in, T* out, long long n, int algo, int exclusive, void* ws, hipStream_t s) {
+    if (n <= 0) return 0;
+    const long long tiles = (n + kTreeTile - 1) / kTreeTile;
+    int blocks = tiles < kRtsBlocks ? (int)tiles : kRtsBlocks;
+    const long long chunk = ((tiles + blocks - 1) / blocks) * kTreeTile;
+    blocks = (int)((n + chunk - 1) / chunk);
+    T* part = (T*)ws;
+    hipLaunchKernelGGL(rts_reduce_kernel<T>, dim3(blocks), dim3(256), 0, s, in, n, chunk, part);
+    hipLaunchKernelGGL(rts_partials_kernel<T>, dim3(1), dim3(1024), 0, s, part, blocks);
+#define TREE(E, A) \
+    hipLaunchKernelGGL((rts_tree_scan_kernel<T, E, A>), dim3(blocks), dim3(256), 0, s, in, out, n, chunk, part)
+    if (algo == 0) {
+        if (exclusive) TREE(true, 0); else TREE(false, 0);
+    } else {
+        if (exclusive) TREE(true, 1); else TREE(false, 1);
+    }
+#undef TREE
+    CME_LAUNCH_STATUS();
+}
+
 // ------------------------------------------------------------ reduction
 template <typename T, typename Op>
 __global__ __launch_bounds__(256) void reduce_partial_kernel(const T* __restrict__ in, long long n, T* __restrict__ part,
@@ -667,6 +786,19 @@ CME_EXPORT int cme_scan_rts(const void* in, void* out, long long n, int dtype, i
     }
 }
 
+// Reduce-then-scan with a tree block scan: algo 0 Blelloch, 1 Hillis-Steele.
+// ws: >= 4 * 1024 bytes.
+CME_EXPORT int cme_scan_tree(const void* in, void* out, long long n, int dtype, int algo, int exclusive, void* ws,
+                             void* stream) {
+    hipStream_t s = as_stream(stream);
+    switch (dtype) {
+        case 0: return launch_tree_rts<float>((const float*)in, (float*)out, n, algo, exclusive, ws, s);
+        case 1: return launch_tree_rts<int>((const int*)in, (int*)out, n, algo, exclusive, ws, s);
+        case 2: return launch_tree_rts<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, algo, exclusive, ws, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
 // dtype: 0 f32, 1 i32, 2 u32. ws: >= 8*ceil(n/4096) + 16 bytes.
 CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -837,4 +969,5 @@ CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* fla
 CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kLbRows>);
 CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
 CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
+CME_REGISTER_KERNEL(scan_blelloch_rts_f32, 256, rts_tree_scan_kernel<float, true, 0>);
 CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true>);

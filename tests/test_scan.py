@@ -92,7 +92,7 @@ def test_generator_and_io_roundtrip(tmp_path):
 @pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 1 << 20, 3_000_001, 9_000_011])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
 @pytest.mark.parametrize("exclusive", [False, True])
-@pytest.mark.parametrize("algo", ["lookback", "rts"])
+@pytest.mark.parametrize("algo", ["lookback", "rts", "blelloch", "hillis"])
 def test_scan_single_pass_gpu(gpu, n, dtype, exclusive, algo):
     x = torch.randint(-3, 4, (n,), dtype=torch.int32).to(dtype)
     ref = np.cumsum(x.numpy().astype(np.int64))
@@ -111,7 +111,7 @@ def test_scan_uint32_gpu(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("algo", ["blelloch", "hillis"])
+@pytest.mark.parametrize("algo", ["blelloch_mlevel", "hillis_mlevel"])
 @pytest.mark.parametrize("n", [5, 512, 513, 262145, 1 << 20])
 def test_scan_mlevel_gpu(gpu, algo, n):
     x = torch.randint(-3, 4, (n,), dtype=torch.int32)
