@@ -278,8 +278,10 @@ struct Stream2 {
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
             const int y = r0 - B + i;
-            const V4<T> o = upd<false>(s1, (S + i) % NW, y);
-            if (y >= y0 && y < y1) {  // wave-uniform
+            // wave-uniform: the first 2B step-2 rows of a chunk are warm-up
+            // (their step-1 window is incomplete) -- skip their arithmetic
+            if (y >= y0 && y < y1) {
+                const V4<T> o = upd<false>(s1, (S + i) % NW, y);
                 T* d = dst + (size_t)y * pitch;
                 if constexpr (!CHECK) {
                     // interior strip: every output lane holds 4 in-region cells
@@ -422,7 +424,7 @@ int stream2_chunk(int strips, int H, int chunk_hint) {
 
 // Two-step pass over `n` output regions `gs` (<= 4, one launch); step-1
 // region `g1` must contain them and extend at most B cells beyond.
-template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
+template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? (FMA ? 2 : 4) : (FMA ? 4 : 2)), int WPE = 1>
 int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl,
                          T ycfl, int chunk_hint, hipStream_t s) {
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
@@ -448,7 +450,7 @@ int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region
     CME_LAUNCH_STATUS();
 }
 
-template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? 2 : (FMA ? 4 : 2)), int WPE = 1>
+template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? (FMA ? 2 : 4) : (FMA ? 4 : 2)), int WPE = 1>
 int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
                    hipStream_t s) {
     return launch_stream2_multi<T, ORDER, FMA, RB, WPE>(prev, curr, pitch, gy, &g, 1, g1, xcfl, ycfl, chunk_hint, s);
