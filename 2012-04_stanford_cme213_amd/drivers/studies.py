@@ -1,7 +1,7 @@
 """Lecture studies as commands (one JSON line per measurement).
 
     python -m cme213x occupancy                       kernel resources + occupancy
-    python -m cme213x study divergence|coalescing|summation
+    python -m cme213x study divergence|coalescing|summation|openmp
 """
 from __future__ import annotations
 
@@ -58,17 +58,30 @@ def summation(device):
         yield {"study": "summation", **{k: (v if k == "n" else float(f"{v:.3e}")) for k, v in row.items()}}
 
 
+def openmp_study():
+    import numpy as np
+
+    from ..ops.studies import omp_schedule_study, omp_sum
+
+    for r in omp_schedule_study():
+        yield {"study": "openmp_schedule", **r}
+    x = np.random.default_rng(0).random(1 << 24)
+    for mode in ("for", "task"):
+        s, sec = omp_sum(x, mode)
+        yield {"study": "openmp_sum", "mode": mode, "seconds": sec, "sum": s}
+
+
 def study_main(argv=None) -> int:
     import torch
 
     ap = argparse.ArgumentParser(prog="cme213x study")
-    ap.add_argument("which", choices=["divergence", "coalescing", "summation"])
+    ap.add_argument("which", choices=["divergence", "coalescing", "summation", "openmp"])
     a = ap.parse_args(argv)
     gpu = torch.cuda.is_available()
-    if a.which != "summation" and not gpu:
+    if a.which in ("divergence", "coalescing") and not gpu:
         print("study needs a GPU")
         return 1
-    gen = {"divergence": divergence_study, "coalescing": coalescing_study}.get(a.which)
+    gen = {"divergence": divergence_study, "coalescing": coalescing_study, "openmp": openmp_study}.get(a.which)
     rows = gen() if gen else summation("cuda" if gpu else None)
     for r in rows:
         print(json.dumps(r), flush=True)

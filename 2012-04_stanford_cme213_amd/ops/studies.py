@@ -16,6 +16,10 @@ from .. import _ext
 _ext.proto(_ext.HIP_PROTOS, "cme_divergence", "pqiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_strided_copy", "ppqiip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_sum_f32", "pqip")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_omp_schedule", "qiiiipp")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_omp_sum", "pqiqpp")
+
+OMP_SCHEDULES = {"static": 0, "static_chunk": 1, "dynamic": 2, "guided": 3}
 
 SUM_ALGOS = {"serial": 0, "pairwise": 1, "kahan": 2}
 
@@ -80,3 +84,28 @@ def summation_study(sizes=(1 << 10, 1 << 14, 1 << 18, 1 << 22, 1 << 24), seed: i
                 row[f"gpu_{algo}"] = abs(float(reduce(xd, "sum", algo)) - exact) / exact
         rows.append(row)
     return rows
+
+
+def omp_schedule_study(n: int = 200_000, work: int = 200, chunk: int = 64, threads: int = 0) -> list[dict]:
+    """OpenMP loop schedules on a triangular (imbalanced) iteration space
+    (slides/Lecture14-15): static blocks leave the last thread with the most
+    work; cyclic chunks, dynamic and guided rebalance."""
+    rows = []
+    for name, code in OMP_SCHEDULES.items():
+        sec = np.zeros(1)
+        chk = np.zeros(1)
+        _ext.call_cpu("cme_cpu_omp_schedule", n, work, code, chunk, threads, sec.ctypes.data, chk.ctypes.data)
+        rows.append({"schedule": name, "chunk": chunk if code else None, "seconds": float(sec[0]),
+                     "checksum": float(chk[0])})
+    return rows
+
+
+def omp_sum(x: np.ndarray, mode: str = "for", cutoff: int = 1 << 16) -> tuple[float, float]:
+    """(sum, seconds) of a float64 array by a parallel-for reduction
+    (``mode="for"``) or recursive OpenMP tasks (``mode="task"``)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.zeros(1)
+    sec = np.zeros(1)
+    _ext.call_cpu("cme_cpu_omp_sum", x.ctypes.data, x.size, 0 if mode == "for" else 1, cutoff, out.ctypes.data,
+                  sec.ctypes.data)
+    return float(out[0]), float(sec[0])

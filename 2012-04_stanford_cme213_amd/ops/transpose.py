@@ -11,10 +11,15 @@ import torch
 from .. import _ext
 
 _ext.proto(_ext.HIP_PROTOS, "cme_transpose_f32", "ppiiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_transpose_reps_f32", "ppiiip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_transpose_f32", "ppiii")
 
 VARIANTS = {"copy": 0, "naive": 1, "lds": 2, "lds_pad": 3, "lds_swizzle": 4, "diagonal": 5, "xcd": 6, "vec": 7,
-            "vec_xcd": 8}
+            "vec_xcd": 8, "naive_1d": 9}
+# the paper's diagnostic kernels (square matrices; NOT transposes):
+# "coarse" moves tiles without transposing their elements, "fine" transposes
+# elements inside tiles that stay in place
+DIAGNOSTICS = {"coarse": 10, "fine": 11}
 
 
 def transpose(x: torch.Tensor, variant: str = "vec", out: torch.Tensor | None = None) -> torch.Tensor:
@@ -35,4 +40,28 @@ def transpose(x: torch.Tensor, variant: str = "vec", out: torch.Tensor | None = 
         else:
             _ext.call_cpu("cme_cpu_transpose_f32", x.data_ptr(), out.data_ptr(), rows, cols,
                           0 if variant == "naive" else 1)
+    return out
+
+
+def diagnostic(x: torch.Tensor, kind: str, out: torch.Tensor | None = None) -> torch.Tensor:
+    """The paper's coarse-/fine-grained diagnostic kernels (square, GPU):
+    ``coarse`` = tiles moved to their transposed position, elements kept in
+    tile order; ``fine`` = elements transposed inside tiles kept in place."""
+    if x.dim() != 2 or x.shape[0] != x.shape[1] or not x.is_cuda:
+        raise ValueError("diagnostics take a square cuda matrix")
+    out = torch.empty_like(x) if out is None else out
+    _ext.call_hip("cme_transpose_f32", x.data_ptr(), out.data_ptr(), x.shape[0], x.shape[1], DIAGNOSTICS[kind],
+                  _ext.stream_ptr(x.device))
+    return out
+
+
+def transpose_reps(x: torch.Tensor, reps: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """lds_pad transpose performed ``reps`` times inside ONE kernel launch --
+    the paper's second timing methodology (launch overhead excluded)."""
+    if not x.is_cuda:
+        raise ValueError("GPU only")
+    rows, cols = x.shape
+    out = torch.empty((cols, rows), dtype=x.dtype, device=x.device) if out is None else out
+    _ext.call_hip("cme_transpose_reps_f32", x.data_ptr(), out.data_ptr(), rows, cols, reps,
+                  _ext.stream_ptr(x.device))
     return out

@@ -155,6 +155,8 @@ def bench_transpose(emit, timeit):
 
     from cme213x.ops.transpose import VARIANTS, transpose
 
+    from cme213x.ops.transpose import DIAGNOSTICS, diagnostic, transpose_reps
+
     ref = {8192: None, 4096: 130.0, 2048: 128.0}  # BASELINE #7/#8 best (LDS+pad+unroll, Fermi)
     for n in (8192, 4096, 2048):
         x = torch.rand(n, n, device="cuda")
@@ -164,6 +166,13 @@ def bench_transpose(emit, timeit):
             gbps = 2 * n * n * 4 / ms / 1e6
             emit(bench="transpose", n=n, variant=v, ms=ms, GBps=gbps, ref_GBps=ref[n],
                  vs_ref=(gbps / ref[n]) if ref[n] else None)
+        for d in DIAGNOSTICS:
+            ms = timeit(lambda: diagnostic(x, d, out))
+            emit(bench="transpose_diag", n=n, kind=d, ms=ms, GBps=2 * n * n * 4 / ms / 1e6)
+        # the paper's two timing modes for the same kernel (lds_pad)
+        reps = 20
+        ms = timeit(lambda: transpose_reps(x, reps, out)) / reps
+        emit(bench="transpose_timing_mode", n=n, mode="loop inside kernel", ms=ms, GBps=2 * n * n * 4 / ms / 1e6)
 
 
 def bench_spmv(emit, timeit):

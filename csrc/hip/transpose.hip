@@ -17,6 +17,14 @@
 //                  and block order from a measured sweep (vec_tile_kernel)
 //                  -- the production variant
 //  8 vec_xcd     : 64x64 vector tile in XCD-aware block order
+//  9 naive_1d    : 1-D grid, one lane per element (the lecture's first rung)
+// 10 coarse      : LDS tile written to its TRANSPOSED tile position but with
+//                  element order unchanged (the paper's "coarse-grained"
+//                  diagnostic: isolates the cost of the tile-level scatter)
+// 11 fine        : elements transposed WITHIN each tile, tile kept in place
+//                  (the paper's "fine-grained" diagnostic)
+// The paper's second timing mode (loop INSIDE the kernel, no launch cost per
+// repetition) is cme_transpose_reps_f32.
 #include "cme213/common.h"
 
 namespace {
@@ -70,6 +78,64 @@ __global__ __launch_bounds__(256) void tile_kernel(const float* __restrict__ in,
     for (int i = 0; i < kT; i += 4) {
         const int oy = x0 + ty + i, ox = y0 + tx;  // output row = input column
         if (oy < cols && ox < rows) out[(size_t)oy * rows + ox] = tile[idx(tx, ty + i)];
+    }
+}
+
+__global__ __launch_bounds__(256) void naive_1d_kernel(const float* __restrict__ in, float* __restrict__ out, int rows,
+                                                       int cols) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    out[(size_t)c * rows + r] = in[i];
+}
+
+// MODE 0 coarse, 1 fine (square matrices; pad-65 LDS tile)
+template <int MODE>
+__global__ __launch_bounds__(256) void grain_kernel(const float* __restrict__ in, float* __restrict__ out, int rows,
+                                                    int cols) {
+    constexpr int P = kT + 1;
+    __shared__ float tile[kT * P];
+    const int tx = threadIdx.x % 64, ty = threadIdx.x / 64;
+    const int x0 = blockIdx.x * kT, y0 = blockIdx.y * kT;
+#pragma unroll 4
+    for (int i = 0; i < kT; i += 4) {
+        const int y = y0 + ty + i, x = x0 + tx;
+        if (y < rows && x < cols) tile[(ty + i) * P + tx] = in[(size_t)y * cols + x];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int i = 0; i < kT; i += 4) {
+        if constexpr (MODE == 0) {  // tile moves, elements keep their order
+            const int oy = x0 + ty + i, ox = y0 + tx;
+            if (oy < cols && ox < rows) out[(size_t)oy * rows + ox] = tile[(ty + i) * P + tx];
+        } else {  // tile stays, elements transposed
+            const int oy = y0 + ty + i, ox = x0 + tx;
+            if (oy < rows && ox < cols) out[(size_t)oy * cols + ox] = tile[tx * P + ty + i];
+        }
+    }
+}
+
+// lds_pad transpose repeated `reps` times inside ONE launch (the paper's
+// in-kernel loop timing mode, my-refs/MatrixTranspose.pdf pp.4-5).
+__global__ __launch_bounds__(256) void tile_reps_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        int rows, int cols, int reps) {
+    constexpr int P = kT + 1;
+    __shared__ float tile[kT * P];
+    const int tx = threadIdx.x % 64, ty = threadIdx.x / 64;
+    const int x0 = blockIdx.x * kT, y0 = blockIdx.y * kT;
+    for (int r = 0; r < reps; ++r) {
+#pragma unroll 4
+        for (int i = 0; i < kT; i += 4) {
+            const int y = y0 + ty + i, x = x0 + tx;
+            if (y < rows && x < cols) tile[(ty + i) * P + tx] = in[(size_t)y * cols + x];
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int i = 0; i < kT; i += 4) {
+            const int oy = x0 + ty + i, ox = y0 + tx;
+            if (oy < cols && ox < rows) out[(size_t)oy * rows + ox] = tile[tx * P + ty + i];
+        }
+        __syncthreads();
     }
 }
 
@@ -187,8 +253,26 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
                 return launch_vec_tile<64, 128, 0>(in, out, rows, cols, s);
             }
             break;
+        case 9:
+            hipLaunchKernelGGL(naive_1d_kernel, dim3(cdiv((size_t)rows * cols, 256)), dim3(256), 0, s, in, out, rows,
+                               cols);
+            break;
+        case 10:
+        case 11:
+            if (rows != cols) return (int)hipErrorInvalidValue;  // diagnostics: square only
+            if (variant == 10)
+                hipLaunchKernelGGL((grain_kernel<0>), grid, dim3(256), 0, s, in, out, rows, cols);
+            else
+                hipLaunchKernelGGL((grain_kernel<1>), grid, dim3(256), 0, s, in, out, rows, cols);
+            break;
         default: return (int)hipErrorInvalidValue;
     }
+    CME_LAUNCH_STATUS();
+}
+
+CME_EXPORT int cme_transpose_reps_f32(const float* in, float* out, int rows, int cols, int reps, void* stream) {
+    dim3 grid(cdiv(cols, kT), cdiv(rows, kT));
+    hipLaunchKernelGGL(tile_reps_kernel, grid, dim3(256), 0, as_stream(stream), in, out, rows, cols, reps);
     CME_LAUNCH_STATUS();
 }
 

@@ -16,6 +16,19 @@ def test_summation_accuracy_ordering():
     assert big["kahan"] < 1e-6
 
 
+def test_openmp_study():
+    import numpy as np
+
+    rows = studies.omp_schedule_study(n=20_000, work=50, chunk=16)
+    assert {r["schedule"] for r in rows} == {"static", "static_chunk", "dynamic", "guided"}
+    chk = {round(r["checksum"], 6) for r in rows}
+    assert len(chk) == 1  # same work under every schedule
+    x = np.random.default_rng(1).random(1 << 20)
+    for mode in ("for", "task"):
+        s, _ = studies.omp_sum(x, mode, cutoff=4096)
+        assert abs(s - x.sum()) < 1e-6 * x.size
+
+
 def test_littles_law():
     from cme213x.utils.occupancy import littles_law
 
