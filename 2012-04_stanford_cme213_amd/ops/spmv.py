@@ -20,6 +20,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_spmv_ell", "iippppfp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_dia", "iiippppfp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_coo", "iqpppppfip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "ipppppifp")
 
 
 # ---------------------------------------------------------------- formats
@@ -43,6 +44,43 @@ class CSR:
         d = torch.zeros(self.nrows, self.ncols)
         d.index_put_((rows, self.col.cpu().long()), self.val.cpu(), accumulate=True)
         return d
+
+
+@dataclass
+class CSRAligned(CSR):
+    """CSR whose rows are zero-padded to multiples of 4 nonzeros, so every row
+    starts on a 16-B boundary (Baskaran & Bordawekar's alignment + padding,
+    ``refs/Baskaran IBM 2009.pdf`` pp.4-8). Padding entries have value 0 and
+    repeat the row's last column index (finite ``x`` assumed)."""
+
+    def to(self, device) -> "CSRAligned":
+        return CSRAligned(self.nrows, self.ncols, self.rp.to(device), self.col.to(device), self.val.to(device))
+
+
+def to_csr_aligned(a: CSR) -> CSRAligned:
+    rp = a.rp.cpu().long()
+    lens = torch.diff(rp)
+    plens = (lens + 3) // 4 * 4
+    prp = torch.zeros(a.nrows + 1, dtype=torch.long)
+    prp[1:] = torch.cumsum(plens, 0)
+    nnz = int(prp[-1])
+    col = torch.zeros(nnz, dtype=torch.int32)
+    val = torch.zeros(nnz, dtype=torch.float32)
+    rows = torch.repeat_interleave(torch.arange(a.nrows), lens)
+    pos = prp[:-1][rows] + (torch.arange(a.nnz) - rp[:-1][rows])
+    col[pos] = a.col.cpu()
+    val[pos] = a.val.cpu()
+    # padding repeats the last real column (or 0 for empty rows)
+    pad_rows = torch.repeat_interleave(torch.arange(a.nrows), plens - lens)
+    if pad_rows.numel():
+        offs = torch.arange(pad_rows.numel()) - torch.repeat_interleave(
+            torch.cumsum(plens - lens, 0) - (plens - lens), plens - lens)
+        ppos = prp[:-1][pad_rows] + lens[pad_rows] + offs
+        last = torch.where(lens[pad_rows] > 0, a.col.cpu().long()[(rp[1:][pad_rows] - 1).clamp(min=0)],
+                           torch.zeros_like(pad_rows))
+        col[ppos] = last.to(torch.int32)
+    dev = a.rp.device
+    return CSRAligned(a.nrows, a.ncols, prp.to(torch.int32).to(dev), col.to(dev), val.to(dev))
 
 
 @dataclass
@@ -238,7 +276,11 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
                       x.data_ptr(), y.data_ptr(), float(beta))
         return y
     s = _ext.stream_ptr(x.device)
-    if isinstance(a, CSR):
+    if isinstance(a, CSRAligned):
+        g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
+        _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), g, float(beta), s)
+    elif isinstance(a, CSR):
         g = 1 if kernel == "scalar" else auto_group(a)
         _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
                       y.data_ptr(), g, float(beta), s)

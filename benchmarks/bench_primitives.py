@@ -178,14 +178,15 @@ def bench_transpose(emit, timeit):
 def bench_spmv(emit, timeit):
     import torch
 
-    from cme213x.ops.spmv import laplacian, random_csr, spmv, to_coo, to_dia, to_ell, to_hyb
+    from cme213x.ops.spmv import laplacian, random_csr, spmv, to_coo, to_csr_aligned, to_dia, to_ell, to_hyb
 
     mats = {"5pt-1M": laplacian("5pt", 1000), "27pt-1M": laplacian("27pt", 100),
             "random-1M": random_csr(1 << 20, 1 << 20, 16, seed=1), "skew-1M": random_csr(1 << 20, 1 << 20, 16,
                                                                                              seed=2, skew=True)}
     for name, a in mats.items():
         x = torch.rand(a.ncols, device="cuda")
-        fmts = {"csr_scalar": a, "csr_vector": a, "coo": to_coo(a), "hyb": to_hyb(a)}
+        fmts = {"csr_scalar": a, "csr_vector": a, "csr_aligned": to_csr_aligned(a), "coo": to_coo(a),
+                "hyb": to_hyb(a)}
         if int((a.rp[1:] - a.rp[:-1]).max()) <= 64:
             fmts["ell"] = to_ell(a)[0]
         if name.startswith(("5pt", "27pt")):

@@ -14,6 +14,11 @@
 //               nonzeros, DPP segmented scan by row, one atomic add per
 //               (row segment x wave) -- load-balanced regardless of row lengths
 //  hyb        : ELL for the first K entries of each row + COO for the rest
+//  csr_aligned: Baskaran's alignment fix (refs/Baskaran IBM 2009.pdf
+//               pp.4-8: rows zero-padded so each starts on a 16-B boundary
+//               and spans whole 4-nnz vectors): G lanes per row, each lane
+//               takes 4 consecutive nonzeros with one 16-B value load and one
+//               16-B index load
 #include "cme213/common.h"
 #include "cme213/wave.h"
 
@@ -43,6 +48,27 @@ __global__ __launch_bounds__(256) void csr_vector_kernel(int nrows, const int* _
     if (r < nrows) {
         const int b = rp[r], e = rp[r + 1];
         for (int j = b + sub; j < e; j += G) s += val[j] * x[col[j]];
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (r < nrows && sub == 0) y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __restrict__ rp,
+                                                       const int* __restrict__ col, const float* __restrict__ val,
+                                                       const float* __restrict__ x, float* __restrict__ y,
+                                                       float beta) {
+    const int r = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    const int sub = threadIdx.x % G;
+    float s = 0.f;
+    if (r < nrows) {
+        const int b = rp[r], e = rp[r + 1];  // multiples of 4 (aligned CSR)
+        for (int j = b + 4 * sub; j < e; j += 4 * G) {
+            const int4 c = *reinterpret_cast<const int4*>(col + j);
+            const float4 v = *reinterpret_cast<const float4*>(val + j);
+            s += v.x * x[c.x] + v.y * x[c.y] + v.z * x[c.z] + v.w * x[c.w];
+        }
     }
 #pragma unroll
     for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -137,6 +163,20 @@ CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const floa
     CME_LAUNCH_STATUS();
 }
 
+// Aligned CSR (every rp[i] % 4 == 0, col/val 16-B aligned): group 1..64.
+CME_EXPORT int cme_spmv_csr_aligned(int nrows, const int* rp, const int* col, const float* val, const float* x,
+                                    float* y, int group, float beta, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (((uintptr_t)col % 16) || ((uintptr_t)val % 16)) return (int)hipErrorInvalidValue;
+    switch (group) {
+#define V(G) case G: hipLaunchKernelGGL(csr_vec4_kernel<G>, dim3(cdiv((size_t)nrows * G, 256)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+        V(1) V(2) V(4) V(8) V(16) V(32) V(64)
+#undef V
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
+
 CME_EXPORT int cme_spmv_ell(int nrows, int K, const int* col, const float* val, const float* x, float* y, float beta,
                             void* stream) {
     hipLaunchKernelGGL(ell_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, as_stream(stream), nrows, K, col, val, x, y,
@@ -166,6 +206,7 @@ CME_EXPORT int cme_spmv_coo(int nrows, long long nnz, const int* row, const int*
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(spmv_csr_scalar, 256, csr_scalar_kernel);
 CME_REGISTER_KERNEL(spmv_csr_vector8, 256, csr_vector_kernel<8>);
+CME_REGISTER_KERNEL(spmv_csr_aligned4, 256, csr_vec4_kernel<4>);
 CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);
 CME_REGISTER_KERNEL(spmv_dia, 256, dia_kernel);
 CME_REGISTER_KERNEL(spmv_coo, 256, coo_kernel);

@@ -3,7 +3,8 @@ import numpy as np
 import pytest
 import torch
 
-from cme213x.ops.spmv import (CSR, hyb_k, laplacian, random_csr, spmv, to_coo, to_dia, to_ell, to_hyb)
+from cme213x.ops.spmv import (CSR, hyb_k, laplacian, random_csr, spmv, to_coo, to_csr_aligned, to_dia, to_ell,
+                               to_hyb)
 
 
 def _ref(a: CSR, x):
@@ -41,7 +42,7 @@ def test_csr_cpu_and_conversions():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
-@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "ell", "dia", "coo", "hyb"])
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_aligned", "ell", "dia", "coo", "hyb"])
 def test_spmv_gpu(gpu, mat, fmt):
     if mat == "5pt":
         a = laplacian("5pt", 100)
@@ -55,7 +56,8 @@ def test_spmv_gpu(gpu, mat, fmt):
         pytest.skip("DIA only for structured matrices")
     x = torch.randn(a.ncols)
     ref = _ref(a, x)
-    dev = {"csr_scalar": a, "csr_vector": a, "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
+    dev = {"csr_scalar": a, "csr_vector": a, "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
+           "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
            "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
     kernel = "scalar" if fmt == "csr_scalar" else "auto"
     y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
