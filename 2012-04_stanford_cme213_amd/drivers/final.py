@@ -1,6 +1,6 @@
 """Final-project drivers.
 
-    python -m cme213x fp a.txt x.txt [check] [--algo lookback|wave|serial]  -> b.txt (+ b_cpu.txt)
+    python -m cme213x fp a.txt x.txt [check] [--algo lookback|wave|serial] [--graph]  -> b.txt (+ b_cpu.txt)
     python -m cme213x checker a.txt x.txt b.txt    (reference_spMVscan-released)
     python -m cme213x readmm <matrix.mtx> <outdir> [q N]   (readMM.py)
     python -m cme213x genfp <name|n p> <outdir> [--q Q] [--iters N]
@@ -22,10 +22,12 @@ def fp_main(argv=None) -> int:
         i = argv.index("--algo")
         algo = argv[i + 1]
         del argv[i:i + 2]
+    graph = "--graph" in argv
+    argv = [a for a in argv if a != "--graph"]
     if len(argv) < 2:
         print('Run command: ./fp "file a.txt" "file x.txt"')
         return 0
-    res = run_fp(argv[0], argv[1], cpu_check=len(argv) >= 3, algo=algo)
+    res = run_fp(argv[0], argv[1], cpu_check=len(argv) >= 3, algo=algo, graph=graph)
     if "relL2" in res:
         print(f"relative L2 error {res['relL2']:g}, relative Linf error {res['relLinf']:g}")
     return 0

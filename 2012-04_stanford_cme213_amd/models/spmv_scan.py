@@ -207,7 +207,7 @@ def errors(ref: np.ndarray, b: np.ndarray) -> dict:
 
 
 def run_fp(a_path: str, x_path: str, cpu_check: bool = False, device: str | None = None,
-           out_path: str = "b.txt", algo: str = "lookback") -> dict:
+           out_path: str = "b.txt", algo: str = "lookback", graph: bool = False) -> dict:
     """The ``./fp a.txt x.txt [check]`` driver (``fp.cu:74-216``)."""
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
     prob = load(a_path, x_path)
@@ -215,9 +215,19 @@ def run_fp(a_path: str, x_path: str, cpu_check: bool = False, device: str | None
     sol = SpmvScanSolver(prob, device, algo)
     sol.run(1)  # warm-up (code object load), then restore a
     sol.reset()
+    runner = None
+    if graph and sol.device.type == "cuda":
+        # record the N-iteration loop as one hipGraph (recording does not
+        # execute it); the timed region is a single replay
+        from ..utils.graphs import GraphRunner
+
+        runner = GraphRunner(lambda: sol.run(), warmup=0)
     t = EventTimer("spmv-scan", device=device if device != "cpu" else None, print_result=False)
     with t:
-        sol.run()
+        if runner is not None:
+            runner()
+        else:
+            sol.run()
     print(f"The running time of my code for {prob.iters} iterations is: {t.ms:g} milliseconds.\n")
     b = sol.a.cpu().numpy()
     res = {"ms": t.ms, "n": prob.n, "p": prob.p, "N": prob.iters,

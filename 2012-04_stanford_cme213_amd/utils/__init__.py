@@ -1,1 +1,1 @@
-from . import params, ulp, timer, gridio, mmio, occupancy  # noqa: F401
+from . import params, ulp, timer, gridio, mmio, occupancy, graphs  # noqa: F401

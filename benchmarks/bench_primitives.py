@@ -92,6 +92,13 @@ def main():
             ms = timeit(lambda: sol.run(), iters=5, warmup=1)
             emit(bench="spmvscan", matrix=name, n=n, p=p, N=N, ms=ms, GBps=12 * n * N / ms / 1e6,
                  ref_ms=REF_MS[name], speedup_vs_ref=REF_MS[name] / ms)
+            # the same N-iteration loop replayed as one hipGraph
+            from cme213x.utils.graphs import GraphRunner
+
+            g = GraphRunner(lambda: sol.run())
+            ms = timeit(g, iters=5, warmup=1)
+            emit(bench="spmvscan_graph", matrix=name, n=n, p=p, N=N, ms=ms, GBps=12 * n * N / ms / 1e6,
+                 ref_ms=REF_MS[name], speedup_vs_ref=REF_MS[name] / ms)
 
     if want("spmvscan_algos"):
         from cme213x.models.spmv_scan import BENCH_SHAPES, REF_MS, SpmvScanSolver, generate
