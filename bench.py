@@ -74,7 +74,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--n", "--grid", dest="n", type=int, default=16384, help="global grid edge (points)")
     ap.add_argument("--order", type=int, default=8)
     ap.add_argument("--method", type=int, default=1, help="1 = 1-D stripes, 2 = 2-D blocks")
     ap.add_argument("--mode", choices=["async", "sync"], default="async")
@@ -86,6 +86,9 @@ def main() -> int:
                     help="timesteps per halo exchange / per HBM pass (2 = temporal blocking, 2B-deep halos)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: run the K-step loop in C++ over a native RCCL communicator")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
+                         "(tests; never the reported number)")
     args = ap.parse_args()
 
     import torch
@@ -103,15 +106,20 @@ def main() -> int:
             print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch under torch.distributed.run",
                   file=sys.stderr)
             return 2
-    comm = init_from_env("cuda")
+    on_gpu = args.device == "cuda"
+    comm = init_from_env(args.device)
     rank = comm.rank
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
 
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
     rccl, native_ok = None, False
-    if comm.size > 1 and args.native != "off":
+    if on_gpu and comm.size > 1 and args.native != "off":
         from cme213x.parallel.rccl import NativeRccl
 
         rccl = NativeRccl()
@@ -120,7 +128,8 @@ def main() -> int:
             native_ok = native_selftest(comm, rccl, dev, args)
     use_native = rccl is not None and native_ok
 
-    sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma))
+    sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
+                   fma=bool(args.fma))
 
     def run(k):
         if use_native:
@@ -129,15 +138,15 @@ def main() -> int:
             sim.run(k)
 
     def barrier_sync():
-        torch.cuda.synchronize(dev)
+        sync()
         comm.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
 
     run(args.warmup)
     barrier_sync()
     t0 = time.perf_counter()
     run(args.steps)
-    torch.cuda.synchronize(dev)
+    sync()
     t1 = time.perf_counter()
     comm.barrier()
     if rccl is not None:
@@ -182,6 +191,7 @@ def main() -> int:
                 + (" fma" if args.fma else " exact"),
                 "fma": bool(args.fma),
                 "tblock": args.tblock,
+                "device": args.device,
                 "loop": "native-rccl" if use_native else ("torch.distributed" if comm.size > 1 else "single"),
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
