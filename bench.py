@@ -122,10 +122,21 @@ def main() -> int:
     if on_gpu and comm.size > 1 and args.native != "off":
         from cme213x.parallel.rccl import NativeRccl
 
-        rccl = NativeRccl()
-        native_ok = True
-        if args.native == "auto":
-            native_ok = native_selftest(comm, rccl, dev, args)
+        # any failure on any rank (communicator setup or the self-test) makes
+        # every rank fall back to the torch.distributed loop together
+        try:
+            rccl = NativeRccl()
+            native_ok = native_selftest(comm, rccl, dev, args) if args.native == "auto" else True
+        except Exception as e:  # noqa: BLE001 - reported, then the portable path runs
+            print(f"bench.py rank {rank}: native RCCL loop unavailable ({e}); using torch.distributed",
+                  file=sys.stderr)
+            native_ok = False
+        agree = torch.tensor([1.0 if native_ok else 0.0], device=dev)
+        comm.allreduce_(agree, "min")
+        native_ok = bool(agree.item() == 1.0)
+        if not native_ok and args.native == "on":
+            print("bench.py: --native on but the native loop failed", file=sys.stderr)
+            return 3
     use_native = rccl is not None and native_ok
 
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
