@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from cme213x.models.spmv_scan import (SpmvScanProblem, SpmvScanSolver, errors, generate, load,
+from cme213x.models.spmv_scan import (SpmvScanSolver, errors, generate, load,
                                       reference_solution, reference_solution_quadratic, run_fp, save)
 from cme213x.ops.scan import head_flags_from_offsets, reduce, scan, segmented_scan
 
