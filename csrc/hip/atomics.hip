@@ -46,11 +46,27 @@ __device__ __forceinline__ int f2ord(float f) {
     return i >= 0 ? i : i ^ 0x7fffffff;
 }
 
+// Hierarchical max (Lecture21): lane -> wave (DPP) -> block (LDS) -> one
+// atomicMax per block on an order-preserving int image of the float. Lanes
+// stream 16-B vectors, four independent loads in flight per iteration.
 __global__ __launch_bounds__(256) void global_max_kernel(const float* __restrict__ in, long long n,
                                                          int* __restrict__ out) {
     __shared__ float lds[4];
     float m = -__builtin_huge_valf();
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m = fmaxf(m, in[i]);
+    const long long n4 = ((uintptr_t)in % 16) ? 0 : n / 4;
+    const float4* in4 = reinterpret_cast<const float4*>(in);
+    const long long stride = (long long)gridDim.x * 256;
+    long long i = blockIdx.x * 256LL + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = in4[i], b = in4[i + stride], c = in4[i + 2 * stride], d = in4[i + 3 * stride];
+        m = fmaxf(m, fmaxf(fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)), fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w))));
+        m = fmaxf(m, fmaxf(fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w)), fmaxf(fmaxf(d.x, d.y), fmaxf(d.z, d.w))));
+    }
+    for (; i < n4; i += stride) {
+        const float4 a = in4[i];
+        m = fmaxf(m, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+    }
+    for (long long j = 4 * n4 + blockIdx.x * 256LL + threadIdx.x; j < n; j += stride) m = fmaxf(m, in[j]);
     const float b = block_reduce<4>(m, lds, OpMax());
     if (threadIdx.x == 0) atomicMax(out, f2ord(b));
 }
@@ -88,7 +104,7 @@ CME_EXPORT int cme_monte_carlo_pi(long long samples, unsigned long long seed, un
 CME_EXPORT int cme_global_max(const float* in, long long n, int* out, void* stream) {
     hipStream_t s = as_stream(stream);
     CME_TRY(hipMemsetAsync(out, 0x80, 4, s));  // 0x80808080: far below any mapped float
-    hipLaunchKernelGGL(global_max_kernel, dim3(stream_grid(n, 256, 4)), dim3(256), 0, s, in, n, out);
+    hipLaunchKernelGGL(global_max_kernel, dim3(stream_grid((n + 15) / 16, 256, 4)), dim3(256), 0, s, in, n, out);
     CME_LAUNCH_STATUS();
 }
 

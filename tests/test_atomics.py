@@ -19,8 +19,12 @@ def test_mc_pi_gpu_matches_cpu_stream(gpu):
 
 @pytest.mark.gpu
 def test_global_max_gpu(gpu):
-    for x in (torch.randn(1_000_003), -torch.rand(5000) - 1.0, torch.tensor([3.5])):
+    for x in (torch.randn(1_000_003), -torch.rand(5000) - 1.0, torch.tensor([3.5]), torch.randn(1 << 24)):
         assert global_max(x.to(gpu)) == float(x.max())
+    # unaligned start (scalar path) and a maximum in the scalar tail
+    x = torch.randn(100_001)
+    x[-1] = 50.0
+    assert global_max(x.to(gpu)[1:]) == 50.0
 
 
 @pytest.mark.gpu
