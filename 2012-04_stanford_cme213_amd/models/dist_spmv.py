@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..ops.spmv import CSR, spmv
+from ..ops.spmv import CSR, spmv, to_csr_aligned, to_ell
 from ..parallel.comm import Comm
 
 
@@ -29,9 +29,25 @@ def nnz_balanced_bounds(rp: np.ndarray, P: int) -> np.ndarray:
     return np.concatenate([[0], cuts, [rp.size - 1]]).astype(np.int64)
 
 
+def _local_format(a: CSR, fmt: str, device):
+    """Local block storage on the GPU: ELL when rows are short (coalesced, no
+    row pointers), else zero-padded aligned CSR (16-B vector loads). The CPU
+    backend takes CSR."""
+    if fmt == "csr" or torch.device(device).type != "cuda":
+        return a
+    lens = torch.diff(a.rp.cpu().long())
+    if fmt == "ell" or (fmt == "auto" and a.nrows and int(lens.max()) <= 32):
+        ell, rest = to_ell(a)
+        if rest.nnz == 0:
+            return ell
+    return to_csr_aligned(a)
+
+
 class RowPartitionedSpMV:
-    def __init__(self, a: CSR, comm: Comm, device, mode: str = "allgather"):
-        """``a``: the full matrix (every rank builds the same partition)."""
+    def __init__(self, a: CSR, comm: Comm, device, mode: str = "allgather", fmt: str = "auto"):
+        """``a``: the full matrix (every rank builds the same partition).
+        ``fmt``: local block format -- "auto" (ELL for short rows, else
+        aligned CSR), "ell", "csr_aligned" or "csr"."""
         self.comm = comm
         self.P, self.r = comm.size, comm.rank
         self.n = a.nrows
@@ -50,7 +66,8 @@ class RowPartitionedSpMV:
         if mode == "allgather":
             # map global column -> padded-gather position (owner*blk + offset)
             gcol = owner * self.blk + (col - self.bounds[owner])
-            self.local = CSR(hi - lo, self.P * self.blk, lrp, torch.from_numpy(gcol.astype(np.int32)), val).to(device)
+            self.local = _local_format(
+                CSR(hi - lo, self.P * self.blk, lrp, torch.from_numpy(gcol.astype(np.int32)), val), fmt, device).to(device)
         elif mode == "halo":
             uniq = np.unique(col)
             uown = np.searchsorted(self.bounds, uniq, side="right") - 1
@@ -72,13 +89,15 @@ class RowPartitionedSpMV:
             self.send_mask = torch.zeros_like(self.send_idx, dtype=torch.bool)
             for q in range(self.P):
                 self.send_mask[q, :self.send_counts[q]] = True
-            # local column ids point into the received halo buffer [P, maxc]
-            pos = {}
-            for q in range(self.P):
-                for j, g in enumerate(need[q]):
-                    pos[int(g)] = q * self.maxc + j
-            lcol = np.fromiter((pos[int(c)] for c in col), dtype=np.int64, count=col.size)
-            self.local = CSR(hi - lo, self.P * self.maxc, lrp, torch.from_numpy(lcol.astype(np.int32)), val).to(device)
+            # local column ids point into the received halo buffer [P, maxc]:
+            # uniq is sorted and grouped by owner, so entry k of uniq lands at
+            # owner*maxc + (k - first index of that owner's group)
+            first = np.searchsorted(uown, np.arange(self.P))
+            upos = uown * self.maxc + (np.arange(uniq.size) - first[uown])
+            lcol = upos[np.searchsorted(uniq, col)]
+            self.local = _local_format(
+                CSR(hi - lo, self.P * self.maxc, lrp, torch.from_numpy(lcol.astype(np.int32)), val), fmt,
+                device).to(device)
         else:
             raise ValueError(mode)
 

@@ -34,3 +34,15 @@ def test_bench_multirank_cpu(nproc, extra):
     assert rec["n_gpus"] == nproc and rec["steps"] == 5 and rec["warmup"] == 1
     assert rec["sanity_ok"] is True and rec["value"] > 0
     assert rec["config"]["loop"] == "torch.distributed"
+
+
+@pytest.mark.parametrize("mode", ["halo", "allgather"])
+def test_dist_spmv_bench_cpu(mode):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "benchmarks", "bench_dist_spmv.py"),
+           "--grid", "64", "--steps", "3", "--warmup", "1", "--device", "cpu", "--mode", mode]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 3 and rec["max_abs_err"] < 1e-4

@@ -161,3 +161,18 @@ def test_two_ranks_one_gpu(gpu, native):
     B = p.border
     for x0, y0, part in parts:
         np.testing.assert_array_equal(part, st[B + y0:B + y0 + part.shape[0], B + x0:B + x0 + part.shape[1]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["halo", "allgather"])
+@pytest.mark.parametrize("fmt", ["auto", "csr", "csr_aligned", "ell"])
+def test_row_partitioned_spmv_gpu_world1(gpu, mode, fmt):
+    from cme213x.models.dist_spmv import RowPartitionedSpMV
+    from cme213x.ops.spmv import laplacian, random_csr, spmv
+    from cme213x.parallel.comm import LoopbackComm
+
+    for a in (laplacian("5pt", 120), random_csr(5000, 5000, 9, seed=3)):
+        x = torch.rand(a.ncols)
+        op = RowPartitionedSpMV(a, LoopbackComm(), gpu, mode=mode, fmt=fmt)
+        y = op(op.local_slice(x).to(gpu)).cpu()
+        torch.testing.assert_close(y, spmv(a, x), rtol=1e-5, atol=1e-5)
