@@ -33,7 +33,20 @@ __global__ __launch_bounds__(256) void csr_scalar_kernel(int nrows, const int* _
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrows) return;
     float s = 0.f;
-    for (int j = rp[r]; j < rp[r + 1]; ++j) s += val[j] * x[col[j]];
+    const int e = rp[r + 1];
+    int j = rp[r];
+    for (; j + 4 <= e; j += 4) {  // 4 index/value loads in flight, then 4 gathers
+        int c[4];
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            c[q] = col[j + q];
+            v[q] = val[j + q];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += v[q] * x[c[q]];
+    }
+    for (; j < e; ++j) s += val[j] * x[col[j]];
     y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
 
@@ -75,15 +88,34 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __r
     if (r < nrows && sub == 0) y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
 
+// All column / value loads of a group of 4 entries are issued before the
+// dependent x gathers (the row loop is a load-latency chain otherwise);
+// padding (col < 0) is masked without a branch. Summation order is k order.
 __global__ __launch_bounds__(256) void ell_kernel(int nrows, int K, const int* __restrict__ col,
                                                   const float* __restrict__ val, const float* __restrict__ x,
                                                   float* __restrict__ y, float beta) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrows) return;
     float s = 0.f;
-    for (int k = 0; k < K; ++k) {
+    int k = 0;
+    for (; k + 4 <= K; k += 4) {
+        int c[4];
+        float v[4], xv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            c[j] = col[(size_t)(k + j) * nrows + r];
+            v[j] = val[(size_t)(k + j) * nrows + r];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] = x[c[j] < 0 ? 0 : c[j]];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += c[j] >= 0 ? v[j] * xv[j] : 0.f;
+    }
+    for (; k < K; ++k) {
         const int c = col[(size_t)k * nrows + r];
-        if (c >= 0) s += val[(size_t)k * nrows + r] * x[c];
+        const float v = val[(size_t)k * nrows + r];
+        const float xv = x[c < 0 ? 0 : c];
+        s += c >= 0 ? v * xv : 0.f;
     }
     y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
@@ -97,9 +129,25 @@ __global__ __launch_bounds__(256) void dia_kernel(int nrows, int ncols, int ndia
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrows) return;
     float s = 0.f;
-    for (int d = 0; d < ndiag; ++d) {
+    int d = 0;
+    for (; d + 4 <= ndiag; d += 4) {  // loads of 4 diagonals in flight
+        int c[4];
+        float v[4], xv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            c[j] = r + (d + j < 64 ? s_off[d + j] : offsets[d + j]);
+            v[j] = data[(size_t)(d + j) * nrows + r];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[j] = x[c[j] < 0 ? 0 : (c[j] >= ncols ? ncols - 1 : c[j])];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += (c[j] >= 0 && c[j] < ncols) ? v[j] * xv[j] : 0.f;
+    }
+    for (; d < ndiag; ++d) {
         const int c = r + (d < 64 ? s_off[d] : offsets[d]);
-        if (c >= 0 && c < ncols) s += data[(size_t)d * nrows + r] * x[c];
+        const float v = data[(size_t)d * nrows + r];
+        const float xv = x[c < 0 ? 0 : (c >= ncols ? ncols - 1 : c)];
+        s += (c >= 0 && c < ncols) ? v * xv : 0.f;
     }
     y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
