@@ -33,7 +33,16 @@ __global__ __launch_bounds__(256) void pr_ref_kernel(const uint32_t* __restrict_
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float sum = 0.f;
-    for (uint32_t j = idx[i]; j < idx[i + 1]; ++j) {
+    const uint32_t e1 = idx[i + 1];
+    uint32_t j = idx[i];
+    for (; j + 4 <= e1; j += 4) {  // loads first, same summation order
+        uint32_t c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = edges[j + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum += in[c[q]] * inv[c[q]];
+    }
+    for (; j < e1; ++j) {
         uint32_t e = edges[j];
         sum += in[e] * inv[e];
     }
@@ -50,7 +59,15 @@ __global__ __launch_bounds__(256) void pr_scalar_kernel(const uint32_t* __restri
     if (i >= n) return;
     const uint32_t b = idx[i], e = idx[i + 1];
     float sum = 0.f;
-    for (uint32_t j = b; j < e; ++j) sum += y_in[edges[j]];
+    uint32_t j = b;
+    for (; j + 4 <= e; j += 4) {  // 4 edge loads in flight, then 4 gathers (same summation order)
+        uint32_t c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = edges[j + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum += y_in[c[q]];
+    }
+    for (; j < e; ++j) sum += y_in[edges[j]];
     float o = 0.5f / (float)n + 0.5f * sum;
     out[i] = o;
     y_out[i] = o * inv[i];
