@@ -52,6 +52,21 @@ def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
     return workspace(x.device, tiles * 8 + 16)
 
 
+def lookback_timed_out(device: torch.device | str = "cuda") -> bool:
+    """True if the last look-back launch on ``device`` hit its bounded-spin
+    limit (its result is then wrong). Reads the workspace timeout word
+    (lookback.h layout: word 0), so it synchronises."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _ws_cache.get(("lookback", idx))
+    return bool(t is not None and int(t[:4].view(torch.int32).item()) != 0)
+
+
+def _check_lookback(x: torch.Tensor) -> None:
+    if _ext.SYNC_CHECK and lookback_timed_out(x.device):
+        raise RuntimeError("look-back scan spin limit exceeded: result invalid")
+
+
 def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
          algo: str = "rts") -> torch.Tensor:
     """Prefix sum of a 1-D contiguous float32/int32/uint32 tensor.
@@ -68,6 +83,7 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
         if algo == "lookback":
             _ext.call_hip("cme_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           _lookback_ws(x).data_ptr(), s)
+            _check_lookback(x)
         elif algo == "rts":
             _ext.call_hip("cme_scan_rts", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           workspace(x.device, 8192, "rts").data_ptr(), s)
@@ -133,6 +149,7 @@ def segmented_scan(x: torch.Tensor, flags: torch.Tensor, out: torch.Tensor | Non
     if x.is_cuda:
         _ext.call_hip("cme_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n,
                       _lookback_ws(x).data_ptr(), _ext.stream_ptr(x.device))
+        _check_lookback(x)
     else:
         _ext.call_cpu("cme_cpu_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n)
     return out
@@ -148,4 +165,5 @@ def spmv_scan_run(a: torch.Tensor, xx: torch.Tensor, flags: torch.Tensor, iters:
     assert flags.dtype == torch.int32, "bitmask flags expected"
     _ext.call_hip("cme_spmv_scan_run", a.data_ptr(), xx.data_ptr(), flags.data_ptr(), a.numel(), iters,
                   _lookback_ws(a).data_ptr(), _ext.stream_ptr(a.device))
+    _check_lookback(a)
     return a

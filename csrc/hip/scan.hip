@@ -741,9 +741,9 @@ int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipSt
     static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows>, kScanThreads);
     const int cap = kNumCU * (exclusive ? bpc_e : bpc_i);
     const int grid = tiles < cap ? tiles : cap;
-    uint64_t* desc = (uint64_t*)ws;
-    unsigned* timeout = (unsigned*)(desc + tiles);
-    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    unsigned* timeout = lb_timeout_word(ws);
+    uint64_t* desc = lb_descriptors(ws);
+    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
     if (exclusive)
         hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows>), dim3(grid), dim3(kScanThreads), 0,
                            s, in, out, n, desc, tiles, timeout);
@@ -825,9 +825,9 @@ CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows,
     else if (rows == 8) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 8, true>, kScanThreads);
     else bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 16, true>, kScanThreads);
     const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    uint64_t* desc = (uint64_t*)ws;
-    unsigned* timeout = (unsigned*)(desc + tiles);
-    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    unsigned* timeout = lb_timeout_word(ws);
+    uint64_t* desc = lb_descriptors(ws);
+    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
 #define ST(R, L)                                                                                                   \
     hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L>), dim3(grid), dim3(kScanThreads), 0, s, in, out, n,  \
                        desc, tiles, timeout)
@@ -913,9 +913,9 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
     const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    uint64_t* desc = (uint64_t*)ws;
-    unsigned* timeout = (unsigned*)(desc + tiles);
-    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    unsigned* timeout = lb_timeout_word(ws);
+    uint64_t* desc = lb_descriptors(ws);
+    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
 #define SEG(M, F) \
     hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, tiles, timeout, 1u)
     if (flag_mode == 0) {
@@ -937,9 +937,9 @@ int spmv_scan_launch(float* a, const float* xx, const uint32_t* flags, long long
     const int tiles = (int)((n + TILE - 1) / TILE);
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF>, kScanThreads);
     const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    uint64_t* desc = (uint64_t*)ws;
-    unsigned* timeout = (unsigned*)(desc + tiles);
-    CME_TRY(hipMemsetAsync(ws, 0, (size_t)tiles * 8 + 16, s));
+    unsigned* timeout = lb_timeout_word(ws);
+    uint64_t* desc = lb_descriptors(ws);
+    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
     for (int it = 0; it < iters; ++it)
         hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a, flags,
                            n, desc, tiles, timeout, (uint32_t)(it + 1));

@@ -6,13 +6,16 @@
 // with a relaxed agent-scope atomic store (global_store ... sc1) and
 // predecessors' granules are re-read with relaxed agent-scope atomic loads
 // (sc1, bypassing the per-CU L1). No fences are needed and results do not
-// depend on dispatch order or XCD placement. Tile ids come from an atomic
-// ticket so every predecessor of a tile is already resident or finished
-// (forward progress without co-residency assumptions). The descriptor array
-// and the ticket are zeroed by the launcher (hipMemsetAsync) before EVERY
-// launch. Spins are bounded: a tile that waits > kSpinLimit polls sets the
-// timeout word and continues (the launcher reports it), so a bug can never
-// hang the GPU.
+// depend on dispatch order or XCD placement. Grids are persistent and
+// co-resident (sized from the occupancy API, common.h
+// persistent_blocks_per_cu); block b scans tiles b, b+G, ... in order, so
+// every predecessor of a tile is owned by a running block (no ordering
+// ticket: a single atomic word saturates at ~88 ops/us). The workspace --
+// timeout word, then the descriptor array -- is zeroed by the launcher
+// (hipMemsetAsync). Spins are bounded: a tile that waits > kSpinLimit polls
+// sets the timeout word and continues, so a bug can never hang the GPU; the
+// Python layer reads the word (ops/scan.py lookback_timed_out; automatic
+// under CME_SYNC_CHECK=1, asserted by the tests).
 #pragma once
 #include "common.h"
 #include "wave.h"
@@ -24,6 +27,11 @@ namespace cme {
 // and gives iteration i epoch i+1 (epoch 0 never matches a zeroed word).
 enum : uint32_t { kStInvalid = 0, kStAggregate = 1, kStInclusive = 2, kStFlag = 4 };
 constexpr unsigned kSpinLimit = 1u << 22;
+
+// Workspace layout: [0, 16) timeout word (+ pad), [16, 16 + 8*tiles) descriptors.
+static inline unsigned* lb_timeout_word(void* ws) { return (unsigned*)ws; }
+static inline uint64_t* lb_descriptors(void* ws) { return (uint64_t*)((char*)ws + 16); }
+static inline size_t lb_ws_bytes(long long tiles) { return 16 + (size_t)tiles * 8; }
 
 __device__ __forceinline__ void lb_publish(uint64_t* d, uint32_t status, uint32_t vbits, uint32_t epoch = 0) {
     __hip_atomic_store(d, ((uint64_t)((epoch << 8) | status) << 32) | vbits, __ATOMIC_RELAXED,

@@ -9,7 +9,7 @@ import torch
 
 from cme213x.models.spmv_scan import (SpmvScanSolver, errors, generate, load,
                                       reference_solution, reference_solution_quadratic, run_fp, save)
-from cme213x.ops.scan import head_flags_from_offsets, reduce, scan, segmented_scan
+from cme213x.ops.scan import head_flags_from_offsets, lookback_timed_out, reduce, scan, segmented_scan
 
 SMALL = "/root/reference/hw/hw_final/programming/aux/CheckOutput"
 
@@ -100,6 +100,8 @@ def test_scan_single_pass_gpu(gpu, n, dtype, exclusive, algo):
         ref = np.concatenate([[0], ref[:-1]])
     y = scan(x.to(gpu), exclusive, algo=algo).cpu().numpy().astype(np.int64)
     np.testing.assert_array_equal(y, ref)  # small integers: exact in fp32 too
+    if algo == "lookback":
+        assert not lookback_timed_out(gpu)
 
 
 @pytest.mark.gpu
@@ -153,6 +155,7 @@ def test_segscan_gpu(gpu, nseg, bitmask):
     f = head_flags_from_offsets(torch.from_numpy(s), n, gpu, bitmask)
     out = segmented_scan(torch.from_numpy(v).to(gpu), f, mul=torch.from_numpy(m).to(gpu)).cpu().numpy()
     np.testing.assert_array_equal(out.astype(np.float64), ref)
+    assert not lookback_timed_out(gpu)
 
 
 @pytest.mark.gpu
