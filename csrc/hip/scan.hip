@@ -72,7 +72,7 @@ __device__ __forceinline__ void store_v4(T* p, long long i, long long n, const V
 // ------------------------------------------------------------ look-back scan
 // ROWS 16-B vectors per lane (tile = 256 * 4 * ROWS elements). LOOKBACK=false
 // is a timing-only diagnostic arm (tiles scanned independently: wrong result).
-template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true>
+template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true, int LBD = 1, bool LATE_PF0 = false>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                      long long n, uint64_t* desc, int tiles,
                                                                      unsigned* timeout) {
@@ -132,10 +132,12 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     }
     if (LOOKBACK && wid == 0 && lane == 0 && tile > 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
     // prefetch the next tile of this block while the look-back resolves
+    // (LATE_PF0: the look-back wave issues its share after the look-back, so
+    // its polls do not queue behind its own prefetch in the vmcnt order)
     Vec4<T> vn[ROWS];
     const int next = tile + gridDim.x;
-    if (next < tiles) {
-        const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
+    const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
+    if (next < tiles && !(LATE_PF0 && LOOKBACK && wid == 0)) {
 #pragma unroll
         for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
     }
@@ -148,11 +150,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
                 s_prefix[parity] = T(0);
             }
         } else {
-            T pre = lb_lookback<T, false>(desc, tile, timeout);
+            T pre = lb_lookback<T, false, LBD>(desc, tile, timeout);
             if (lane == 0) {
                 lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
                 s_prefix[parity] = pre;
             }
+        }
+        if (LATE_PF0 && next < tiles) {
+#pragma unroll
+            for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
         }
     }
     __syncthreads();
@@ -815,6 +821,11 @@ CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1
 // Diagnostic/tuning arms of the look-back scan (f32 exclusive): rows = 4/8/16
 // vectors per lane, lookback = 0 skips the cross-tile pass (wrong results;
 // isolates the hand-off cost).
+// Tuning arms. lookback: 0 off (timing only, wrong result); 1 persistent
+// co-resident grid (production); 2 one tile per block (grid = tiles, relies on
+// in-order workgroup dispatch for forward progress); 3/4 as 1/2 with a 2-wide
+// look-back window per lane; 5 persistent at half the co-resident grid;
+// 6 persistent with the look-back wave prefetching after its look-back.
 CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows, int lookback, void* ws,
                              void* stream) {
     hipStream_t s = as_stream(stream);
@@ -824,17 +835,29 @@ CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows,
     if (rows == 4) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 4, true>, kScanThreads);
     else if (rows == 8) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 8, true>, kScanThreads);
     else bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 16, true>, kScanThreads);
-    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
+    if (lookback == 5) bpc = bpc > 1 ? bpc / 2 : 1;
+    int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
+    if (lookback == 2 || lookback == 4) grid = tiles;
     unsigned* timeout = lb_timeout_word(ws);
     uint64_t* desc = lb_descriptors(ws);
     CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
-#define ST(R, L)                                                                                                   \
-    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L>), dim3(grid), dim3(kScanThreads), 0, s, in, out, n,  \
-                       desc, tiles, timeout)
-    if (rows == 4) { if (lookback) ST(4, true); else ST(4, false); }
-    else if (rows == 8) { if (lookback) ST(8, true); else ST(8, false); }
-    else if (rows == 16) { if (lookback) ST(16, true); else ST(16, false); }
+#define ST(R, L, D)                                                                                                \
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D>), dim3(grid), dim3(kScanThreads), 0, s, in, out, \
+                       n, desc, tiles, timeout)
+#define ST6(R)                                                                                                    \
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, true, 1, true>), dim3(grid), dim3(kScanThreads), 0, s, \
+                       in, out, n, desc, tiles, timeout)
+#define SR(R)                                                    \
+    if (lookback == 0) ST(R, false, 1);                          \
+    else if (lookback == 3 || lookback == 4) ST(R, true, 2);     \
+    else if (lookback == 6) ST6(R);                              \
+    else ST(R, true, 1);
+    if (rows == 4) { SR(4) }
+    else if (rows == 8) { SR(8) }
+    else if (rows == 16) { SR(16) }
     else return (int)hipErrorInvalidValue;
+#undef SR
+#undef ST6
 #undef ST
     CME_LAUNCH_STATUS();
 }
