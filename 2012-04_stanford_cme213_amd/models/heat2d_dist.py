@@ -34,7 +34,7 @@ import time
 import numpy as np
 import torch
 
-from ..ops.stencil import heat_step, heat_step2
+from ..ops.stencil import heat_step, heat_stepn
 from ..parallel.comm import Comm, LoopbackComm, P2P, Pending
 from ..parallel.decomp import Block, decompose
 from ..utils.params import SimParams
@@ -131,8 +131,10 @@ class DistHeat:
         self.local_ranks = local_ranks if local_ranks is not None else [self.comm.rank]
         if self.comm.size > 1 and (len(self.local_ranks) != 1 or self.world != self.comm.size):
             raise ValueError("multi-process runs own exactly one subdomain per rank")
-        if tblock not in (1, 2):
-            raise ValueError("tblock must be 1 or 2")
+        if tblock not in (1, 2, 3, 4):
+            raise ValueError("tblock must be 1..4")
+        if tblock > 2 and dtype == torch.float64 and torch.device(device).type == "cuda":
+            raise ValueError("tblock 3/4 (3- and 4-step passes) is fp32 only on the GPU")
         self.fma = bool(fma)
         self.variant = "fma" if self.fma else variant
         self.tblock = tblock
@@ -232,21 +234,28 @@ class DistHeat:
         self.iteration += 1
 
     def step2(self, sync: bool | None = None) -> None:
-        """TWO timesteps per exchange (``tblock=2``): 2B-deep halos (corners
-        included) feed one fused two-step pass per region; the deep interior
-        (2B from any neighbour) overlaps the in-flight exchange in async mode.
-        Same schedule as the native loop (``csrc/hip/dist_heat.hip``)."""
-        if self.tblock != 2:
-            raise ValueError("step2 needs tblock=2 (2B-deep halos)")
+        """TWO timesteps per exchange (needs ``tblock >= 2``)."""
+        self.stepn(2, sync)
+
+    def stepn(self, ns: int, sync: bool | None = None) -> None:
+        """``ns`` timesteps per exchange (``2 <= ns <= tblock``): the
+        ``tblock*B``-deep halos (corners included) feed one fused ``ns``-step
+        pass per region; the deep interior (``tblock*B`` from any neighbour)
+        overlaps the in-flight exchange in async mode, and the border strips go
+        out as one launch. Same schedule as the native loop
+        (``csrc/hip/dist_heat.hip``)."""
+        if not 2 <= ns <= self.tblock:
+            raise ValueError(f"stepn({ns}) needs 2 <= ns <= tblock={self.tblock}")
         sync = self.p.sync if sync is None else sync
         k = self._cur()
 
         def sweep(regions_of):
             for s in self.subs.values():
                 g = s.grid
-                ext = _ext_region(s)
-                for reg in regions_of(s, 2 * g.B):
-                    heat_step2(g.buf[k], g.buf[1 - k], reg, ext, g.order, g.xcfl, g.ycfl, fma=self.fma)
+                regs = list(regions_of(s, self.tblock * g.B))
+                if regs:
+                    heat_stepn(g.buf[k], g.buf[1 - k], regs, _ext_region(s), g.order, g.xcfl, g.ycfl, ns,
+                               fma=self.fma)
 
         if sync:
             sweep(_interior_regions)
@@ -261,8 +270,8 @@ class DistHeat:
             self._pending = self.exchange(1 - k)
         for s in self.subs.values():
             s.grid.cur = 1 - k
-            s.grid.iteration += 2
-        self.iteration += 2
+            s.grid.iteration += ns
+        self.iteration += ns
 
     # -- native loop (RCCL + HIP, no per-step Python) ---------------------
     def _sub_plan(self, r: int, s: _Sub) -> dict:
@@ -326,9 +335,9 @@ class DistHeat:
     def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None) -> None:
         """``iters`` timesteps in ONE native call (``cme_heat_dist_run``):
         border strips on their own stream, the halo exchange posted as soon
-        as they finish, the deep interior overlapping both; with ``tblock=2``
-        each exchange of 2B-deep halos feeds two timesteps done in one HBM
-        pass. ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl` (one
+        as they finish, the deep interior overlapping both; with ``tblock=n``
+        (2-4) each exchange of nB-deep halos feeds n timesteps done in one
+        HBM pass. ``rccl``: a :class:`~cme213x.parallel.rccl.NativeRccl` (one
         subdomain per process); ``None`` = loopback transport, every
         neighbour being another local subdomain (device copies) -- the same
         stream/event schedule, testable on one GPU. ``transport=2`` skips
@@ -363,10 +372,10 @@ class DistHeat:
 
     def run(self, iters: int, sync: bool | None = None) -> None:
         i = 0
-        if self.tblock == 2:
-            while i + 1 < iters:
-                self.step2(sync)
-                i += 2
+        while iters - i >= 2 and self.tblock >= 2:
+            ns = min(self.tblock, iters - i)
+            self.stepn(ns, sync)
+            i += ns
         for _ in range(i, iters):
             self.step(sync)
         self.finish()
@@ -483,12 +492,15 @@ def _border_regions(s: _Sub, depth: int):
 
 
 def _ext_region(s: _Sub):
-    """Region of the intermediate step of a two-step pass: owned region grown
-    by B into the (2B-deep) halo on every neighbour side."""
+    """Region of the intermediate steps of a multi-step pass: the owned region
+    grown by ``H - B`` (= (tblock-1)*B) into the halo on every neighbour side
+    -- the dependency cone of the first intermediate step; later steps need
+    less. Physical-BC sides stay fixed."""
     g, b = s.grid, s.blk
     H, B = g.H, g.B
-    return (H - B if b.left >= 0 else H, H + g.nx + B if b.right >= 0 else H + g.nx,
-            H - B if b.bottom >= 0 else H, H + g.ny + B if b.top >= 0 else H + g.ny)
+    D = H - B
+    return (H - D if b.left >= 0 else H, H + g.nx + D if b.right >= 0 else H + g.nx,
+            H - D if b.bottom >= 0 else H, H + g.ny + D if b.top >= 0 else H + g.ny)
 
 
 def run_hw5(params_path: str, comm: Comm | None = None, dtype=torch.float64, device: str | None = None,

@@ -20,6 +20,9 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f32", "ppiiiiiiiiffiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_f64", "ppiiiiiiiiddiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiipipiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiipipiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f32", "ppiipipiiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f64", "ppiipipiiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
@@ -29,12 +32,15 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f64", "ppiiiiiidd")
 
 VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
-            "stream2_fma": 5, "stream_fma": 6, "fma": 6}
-# variants that advance more than one timestep per launch (multi-step drivers only)
-MULTISTEP = {"stream2", "stream2_fma"}
+            "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,
+            "stream4_fma": 10}
+# variants that advance more than one timestep per launch (multi-step drivers
+# only); stream3/stream4 (3 / 4 steps per HBM pass) are fp32 only
+MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma"}
+FP32_ONLY = {"stream3", "stream3_fma", "stream4", "stream4_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
-FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma"}
+FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -92,6 +98,48 @@ def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, i
                   order, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
 
 
+def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, int, int, int], order: int,
+               xcfl: float, ycfl: float, nsteps: int, chunk: int = 0, fma: bool = False) -> None:
+    """``nsteps`` (2-4) timesteps in one HBM pass (temporal blocking): the
+    intermediate steps cover ``ext`` (the output regions grown by at most
+    (nsteps-1)*B cells, e.g. into an nsteps*B-deep halo), the last one writes
+    ``curr`` on every region of ``regions`` (one tuple or a list of <= 4, one
+    launch). Cells of ``ext`` outside the grid's update set keep their value.
+    Bitwise equal to ``nsteps`` single steps; 3 and 4 steps are fp32 only.
+    On CPU it runs exactly those single steps through temporaries."""
+    _check(prev, curr)
+    if isinstance(regions[0], int):
+        regions = [regions]
+    if not 1 <= len(regions) <= 4:
+        raise ValueError("1 to 4 output regions per pass")
+    if nsteps == 1:
+        for reg in regions:
+            heat_step(prev, curr, reg, order, xcfl, ycfl, "fma" if fma else ("stream" if prev.is_cuda else "naive"))
+        return
+    if not 2 <= nsteps <= 4:
+        raise ValueError("nsteps must be 1..4")
+    if not prev.is_cuda:
+        v = "fma" if fma else "naive"
+        src = prev
+        for _ in range(nsteps - 1):
+            tmp = prev.clone()
+            heat_step(src, tmp, ext, order, xcfl, ycfl, v)
+            src = tmp
+        for reg in regions:
+            heat_step(src, curr, reg, order, xcfl, ycfl, v)
+        return
+    f64 = prev.dtype == torch.float64
+    if f64 and nsteps > 2:
+        raise ValueError("3- and 4-step passes are fp32 only")
+    rows, pitch = prev.shape
+    flat = [int(v) for reg in regions for v in reg]
+    r = (ctypes.c_int * len(flat))(*flat)
+    e = (ctypes.c_int * 4)(*map(int, ext))
+    name = "cme_heat_stepn_f64" if f64 else "cme_heat_stepn_f32"
+    _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), len(regions),
+                  ctypes.addressof(e), order, nsteps, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
+
+
 def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
              ycfl: float, iters: int, variant: str = "stream", chunk: int = 0) -> torch.Tensor:
     """``iters`` timesteps starting from ``a``; returns the buffer holding the
@@ -102,6 +150,8 @@ def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int]
     xb, xe, yb, ye = map(int, region)
     rows, pitch = a.shape
     f64 = a.dtype == torch.float64
+    if f64 and variant in FP32_ONLY:
+        raise ValueError(f"variant {variant!r} is fp32 only")
     if a.is_cuda:
         name = "cme_heat_run_f64" if f64 else "cme_heat_run_f32"
         final = ctypes.c_int(0)

@@ -10,9 +10,10 @@ EXACTLY K timed steps bracketed by barrier + synchronize, max over ranks; rank
 A "step" is one full timestep of the global grid: the FTCS sweep of every
 point plus the halo exchange between neighbouring ranks (1-D stripes, async
 mode: deep interior overlapped with the exchange, borders after it). With
-``--tblock 2`` (default) two timesteps are fused into one HBM pass
-(temporal blocking) and each exchange moves 2B-deep halos; K timed steps are
-still exactly K timesteps (an odd K ends with one single step).
+``--tblock 3`` (default) three timesteps are fused into one HBM pass
+(temporal blocking) and each exchange moves 3B-deep halos; K timed steps are
+still exactly K timesteps (a K that is not a multiple of 3 ends with a shorter
+pass).
 
 Metric convention: effective GB/s = points x 72 B (17 taps + 1
 store, fp32) per iteration / time -- the convention the reference's 240 GB/s
@@ -82,8 +83,8 @@ def main() -> int:
     ap.add_argument("--fma", type=int, choices=[0, 1], default=1,
                     help="FMA-contracted stencil (what nvcc emits for the reference's GPU kernels); 0 = exact "
                          "contraction-off arithmetic, bitwise equal to the non-FMA CPU oracle")
-    ap.add_argument("--tblock", type=int, choices=[1, 2], default=2,
-                    help="timesteps per halo exchange / per HBM pass (2 = temporal blocking, 2B-deep halos)")
+    ap.add_argument("--tblock", type=int, choices=[1, 2, 3, 4], default=3,
+                    help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: run the K-step loop in C++ over a native RCCL communicator")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -198,7 +199,7 @@ def main() -> int:
                 "global_batch": pts,
                 "seq_len": 1,
                 "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
-                "variant": (args.variant if args.tblock == 1 else "stream2 (2 steps/pass)")
+                "variant": (args.variant if args.tblock == 1 else f"stream{args.tblock} ({args.tblock} steps/pass)")
                 + (" fma" if args.fma else " exact"),
                 "fma": bool(args.fma),
                 "tblock": args.tblock,

@@ -21,11 +21,11 @@ extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int 
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream);
 extern "C" int cme_heat_step_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, double xcfl, double ycfl, int chunk, void* stream);
-extern "C" int cme_heat_step2_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
-                                  const int* ext, int order, float xcfl, float ycfl, int chunk, int fma,
+extern "C" int cme_heat_stepn_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
                                   void* stream);
-extern "C" int cme_heat_step2_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
-                                  const int* ext, int order, double xcfl, double ycfl, int chunk, int fma,
+extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
 
 #define CME_TRY_INT(expr)                 \
@@ -168,20 +168,20 @@ int step_region<double>(const double* p, double* c, int pitch, int gy, const int
     return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
 }
 
-// two-step pass over n (<= 4) regions in one launch
+// ns-step pass (ns = 2..4) over n (<= 4) regions in one launch
 template <typename T>
-int step2_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, T xcfl,
-                  T ycfl, int fma, hipStream_t s);
+int stepn_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, int ns,
+                  T xcfl, T ycfl, int fma, hipStream_t s);
 
 template <>
-int step2_regions<float>(const float* p, float* c, int pitch, int gy, const int* r, int n, const int* ext, int order,
-                         float xcfl, float ycfl, int fma, hipStream_t s) {
-    return cme_heat_step2_f32(p, c, pitch, gy, r, n, ext, order, xcfl, ycfl, 0, fma, (void*)s);
+int stepn_regions<float>(const float* p, float* c, int pitch, int gy, const int* r, int n, const int* ext, int order,
+                         int ns, float xcfl, float ycfl, int fma, hipStream_t s) {
+    return cme_heat_stepn_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma, (void*)s);
 }
 template <>
-int step2_regions<double>(const double* p, double* c, int pitch, int gy, const int* r, int n, const int* ext,
-                          int order, double xcfl, double ycfl, int fma, hipStream_t s) {
-    return cme_heat_step2_f64(p, c, pitch, gy, r, n, ext, order, xcfl, ycfl, 0, fma, (void*)s);
+int stepn_regions<double>(const double* p, double* c, int pitch, int gy, const int* r, int n, const int* ext,
+                          int order, int ns, double xcfl, double ycfl, int fma, hipStream_t s) {
+    return cme_heat_stepn_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma, (void*)s);
 }
 
 // ------------------------------------------------------------- distributed loop
@@ -195,7 +195,7 @@ struct SubDesc {
     int n_int;
     const int* border;    // n_b x {xb, xe, yb, ye}
     int n_b;
-    const int* ext;       // {xb, xe, yb, ye} step-1 region of two-step passes
+    const int* ext;       // {xb, xe, yb, ye} intermediate-step region of multi-step passes
     const long long* rows;  // n_rows x {peer, send_off, recv_off, count} (elements)
     int n_rows;
     const int* blks;      // n_blks x {peer, send_x, send_y, recv_x, recv_y, rows, width}
@@ -351,7 +351,7 @@ int local_peers(const SubDesc* subs, int nsub, int si, int* out) {
     return n;
 }
 
-// The time loop. Per pass i (one or two timesteps), for every sub:
+// The time loop. Per pass i (1..tblock timesteps), for every sub:
 //   border stream : wait halos of p (own comm event, + pulling neighbours'
 //                   in loopback) and the previous interior; border strips;
 //                   record ev_border[i&1]
@@ -366,6 +366,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
              int cur, int sync, int exchange_first, int tblock, int fma, int* cur_out, hipStream_t s) {
     if (nsub < 1 || nsub > kMaxSubs) return (int)hipErrorInvalidValue;
     if (transport == 0 && nsub != 1) return (int)hipErrorInvalidValue;
+    if (tblock < 1 || tblock > 4 || (tblock > 2 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
     // 0 (default): border stream || interior stream; 1: border then interior
     // on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for
@@ -388,13 +389,13 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         if (transport == 1) return post_exchange_loopback<T>(subs, nsub, si, k, ctx->sub[si].comm);
         return 0;  // transport 2: no exchange (benchmarking the compute schedule)
     };
-    auto sweep = [&](int si, const int* regs, int n, int k, bool two, hipStream_t st) -> int {
+    auto sweep = [&](int si, const int* regs, int n, int k, int ns, hipStream_t st) -> int {
         const SubDesc& d = subs[si];
         const T* p = (const T*)d.buf[k];
         T* c = (T*)d.buf[k ^ 1];
         if (n == 0) return 0;
-        if (two)  // all regions (e.g. the 2-4 border strips) in ONE launch
-            return step2_regions<T>(p, c, d.pitch, d.gy, regs, n, d.ext, order, xcfl, ycfl, fma, st);
+        if (ns > 1)  // all regions (e.g. the 2-4 border strips) in ONE launch
+            return stepn_regions<T>(p, c, d.pitch, d.gy, regs, n, d.ext, order, ns, xcfl, ycfl, fma, st);
         for (int i = 0; i < n; ++i) {
             int rc = step_region<T>(p, c, d.pitch, d.gy, regs + 4 * i, order, xcfl, ycfl, fma, st);
             if (rc) return rc;
@@ -417,13 +418,15 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     }
     int pass = 0;
     for (int it = 0; it < iters; ++pass) {
-        const bool two = tblock == 2 && it + 1 < iters;
+        // timesteps in this pass: tblock, or what is left (a tail pass of
+        // fewer steps reuses the tblock*B-deep halos and regions)
+        const int ns = (iters - it) < tblock ? (iters - it) : tblock;
         const int par = pass & 1;
         if (sync) {
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
-                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
-                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
             for (int si = 0; si < nsub; ++si) {
@@ -448,7 +451,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 CME_TRY(hipStreamWaitEvent(u.compute, u.ev_comm, 0));
                 for (int j = 0; j < npeer[si]; ++j)
                     CME_TRY(hipStreamWaitEvent(u.compute, ctx->sub[peers[si][j]].ev_comm, 0));
-                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
             for (int si = 0; si < nsub; ++si) {
@@ -461,7 +464,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
             }
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
-                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
             }
         } else {
@@ -471,7 +474,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 for (int j = 0; j < npeer[si]; ++j)
                     CME_TRY(hipStreamWaitEvent(u.border, ctx->sub[peers[si][j]].ev_comm, 0));
                 CME_TRY(hipStreamWaitEvent(u.border, u.ev_int[par ^ 1], 0));
-                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, two, u.border));
+                CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.border));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.border));
             }
             for (int si = 0; si < nsub; ++si) {  // halo exchange of the new state
@@ -485,12 +488,12 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
             for (int si = 0; si < nsub; ++si) {  // deep interior, overlapping both
                 SubCtx& u = ctx->sub[si];
                 CME_TRY(hipStreamWaitEvent(u.compute, u.ev_border[par ^ 1], 0));
-                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, two, u.compute));
+                CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
             }
         }
         cur ^= 1;
-        it += two ? 2 : 1;
+        it += ns;
     }
     // the caller's stream resumes after every stream of every sub
     for (int si = 0; si < nsub; ++si) {
@@ -510,9 +513,9 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
 // The distributed heat loop (see dist_run). transport 0 = RCCL (`comm`, one
 // sub), 1 = loopback (every neighbour is one of `subs`), 2 = none (halos are
 // not exchanged; benchmarks/bench_dist_rank.py). dtype 0 f32, 1 f64.
-// tblock 1: one step per exchange; 2: two steps per exchange (2B-deep halos,
-// `interior` shrunk by 2B on neighbour sides, `ext` = owned region grown by B
-// on neighbour sides). fma: FMA-contracted stencil.
+// tblock n (1-4): n steps per exchange (nB-deep halos, `interior` shrunk by
+// nB on neighbour sides, `ext` = owned region grown by (n-1)B on neighbour
+// sides; 3 and 4 fp32 only). fma: FMA-contracted stencil.
 CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, int nsub, int dtype, int order,
                                  double xcfl, double ycfl, int iters, int cur, int sync, int exchange_first,
                                  int tblock, int fma, int* cur_out, void* stream) {

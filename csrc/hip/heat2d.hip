@@ -385,6 +385,207 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
                                              xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
 }
 
+// ---------------------------------------------------------------- streamN
+// Deeper temporal blocking: NS (3 or 4) timesteps per HBM pass, the stream2
+// design generalised. The two-step kernel moves 4 B/pt/step and runs at
+// ~4.4 TB/s on 16384^2, short of loads in flight rather than of VALU issue,
+// so the lever is fewer HBM bytes per timestep: NS steps per pass move
+// 8/NS B/pt.
+//
+// Window k (0 = input, k = 1..NS-1 = step-k rows) holds NW = RB + 2B rows in a
+// ring; logical slot j of window k is row r0 - (k+1)B + j. A phase loads RB
+// new input rows, produces RB rows of every step k from window k-1 (rows
+// r0 - (k-1)B + i) and stores RB final rows (y = r0 - (NS-1)B + i). Step k is
+// valid on lanes k..63-k (x-neighbours arrive through DPP), so a strip emits
+// (64 - 2NS) x 4 columns. Rows of step k outside [y0 - (NS-k)B, y1 +
+// (NS-k)B) feed no stored value: their arithmetic is skipped (wave-uniform).
+// Intermediate cells outside the `ext` region keep their input value (fixed
+// boundary cells), so the result equals NS single steps bit for bit.
+template <int NS>
+struct StripN {
+    static constexpr int kOut = (64 - 2 * NS) * 4;
+};
+
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK>
+struct StreamN {
+    static constexpr int B = HeatOrder<ORDER>::B;
+    static constexpr int NW = RB + 2 * B;
+    static constexpr int P = NW / cgcd(NW, RB);
+
+    V4<T> w[NS][NW];
+    V4<T> nxt[RB];
+    const T* src;
+    T* dst;
+    int pitch, gy, xbase;
+    bool out_lane, full_vec;
+    int y0, y1, xb, xe, xb1, xe1, yb1, ye1;
+    T xcfl, ycfl;
+    int r0;
+
+    __device__ __forceinline__ const T* row_ptr(int r) const {
+        r = r < 0 ? 0 : (r >= gy ? gy - 1 : r);
+        return src + (size_t)r * pitch;
+    }
+
+    template <bool MASK>
+    __device__ __forceinline__ V4<T> upd(const V4<T> (&win)[NW], int s_lo, int row) const {
+        const V4<T> c = win[(s_lo + B) % NW];
+        const V4<T> L = wave_shr1(c);
+        const V4<T> R = wave_shl1(c);
+        T rowv[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            rowv[j] = L[j];
+            rowv[4 + j] = c[j];
+            rowv[8 + j] = R[j];
+        }
+        bool row_in = true;
+        if constexpr (MASK) row_in = row >= yb1 && row < ye1;
+        V4<T> o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                xm[k] = rowv[4 + j - (k + 1)];
+                xp[k] = rowv[4 + j + (k + 1)];
+                ym[k] = win[(s_lo + B - (k + 1)) % NW][j];
+                yp[k] = win[(s_lo + B + (k + 1)) % NW][j];
+            }
+            const T u = heat_update_sel<ORDER, FMA>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+            if constexpr (MASK) {
+                const int x = xbase + j;
+                o[j] = (row_in && x >= xb1 && x < xe1) ? u : c[j];
+            } else {
+                o[j] = u;
+            }
+        }
+        return o;
+    }
+
+    // the RB rows of intermediate step K produced in this phase
+    template <int K, int S>
+    __device__ __forceinline__ void inter() {
+        if constexpr (K < NS) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+                const int row = r0 - (K - 1) * B + i;
+                if (row >= y0 - (NS - K) * B && row < y1 + (NS - K) * B)
+                    w[K][(S + 2 * B + i) % NW] = upd<CHECK>(w[K - 1], (S + i) % NW, row);
+            }
+            inter<K + 1, S>();
+        }
+    }
+
+    template <int PH>
+    __device__ __forceinline__ bool phase() {
+        if (r0 - (NS - 1) * B >= y1) return false;
+        constexpr int S = (PH * RB) % NW;
+#pragma unroll
+        for (int i = 0; i < RB; ++i) w[0][(S + 2 * B + i) % NW] = nxt[i];
+        if (r0 + RB < y1 + (NS - 1) * B) {
+#pragma unroll
+            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
+        }
+        inter<1, S>();
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+            const int y = r0 - (NS - 1) * B + i;
+            if (y >= y0 && y < y1) {
+                const V4<T> o = upd<false>(w[NS - 1], (S + i) % NW, y);
+                T* d = dst + (size_t)y * pitch;
+                if constexpr (!CHECK) {
+                    if (out_lane) store4(d, o);
+                } else if (out_lane) {
+                    if (full_vec) {
+                        store4(d, o);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (xbase + j >= xb && xbase + j < xe) d[j] = o[j];
+                    }
+                }
+            }
+        }
+        r0 += RB;
+        if constexpr (PH + 1 < P)
+            return phase<PH + 1>();
+        else
+            return true;
+    }
+
+    __device__ __forceinline__ void run() {
+        r0 = y0 - (NS - 1) * B;
+#pragma unroll
+        for (int i = 0; i < 2 * B; ++i) w[0][i] = load4(row_ptr(r0 - B + i));
+#pragma unroll
+        for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + B + i));
+        while (phase<0>()) {
+        }
+    }
+};
+
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK>
+__device__ __forceinline__ void streamn_run(const T* src, T* dst, int pitch, int gy, int xbase, bool out_lane,
+                                            bool full_vec, int y0, int y1, int xb, int xe, int xb1, int xe1, int yb1,
+                                            int ye1, T xcfl, T ycfl) {
+    StreamN<T, ORDER, RB, NS, FMA, CHECK> st;
+    st.src = src;
+    st.dst = dst;
+    st.pitch = pitch;
+    st.gy = gy;
+    st.xbase = xbase;
+    st.out_lane = out_lane;
+    st.full_vec = full_vec;
+    st.y0 = y0;
+    st.y1 = y1;
+    st.xb = xb;
+    st.xe = xe;
+    st.xb1 = xb1;
+    st.xe1 = xe1;
+    st.yb1 = yb1;
+    st.ye1 = ye1;
+    st.xcfl = xcfl;
+    st.ycfl = ycfl;
+    st.run();
+}
+
+template <typename T, int ORDER, int RB, int NS, bool FMA, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_streamn_kernel(
+    const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
+    int ye1, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int OUT = StripN<NS>::kOut;
+    const int lane = lane_id();
+    int wave = (int)blockIdx.x * 4 + (int)(threadIdx.x / 64);
+    if (wave >= R.wave_end[R.n - 1]) return;
+    int r = 0;
+    while (wave >= R.wave_end[r]) ++r;  // wave-uniform, <= 3 steps
+    if (r > 0) wave -= R.wave_end[r - 1];
+    const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
+    const int strips = R.strips[r], chunk = R.chunk[r];
+    const int strip = wave % strips;
+    const int ck = wave / strips;
+    const int y0 = yb + ck * chunk;
+    const int y1 = min(ye, y0 + chunk);
+    const int xs = (xb & ~3) + strip * OUT;
+    const int xbase = xs - 4 * NS + 4 * lane;
+    const int xl = min(max(xbase, 0), pitch - 4);
+    const bool out_lane = (lane >= NS) && (lane <= 63 - NS) && (xbase < xe) && (xbase + 4 > xb);
+    const bool full_vec = (xbase >= xb) && (xbase + 4 <= xe);
+    // every intermediate cell that feeds a stored value lies inside ext, and
+    // every output column inside [xb, xe): no per-cell selects
+    constexpr int reach = 4 * (NS - 1);
+    const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
+                        (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
+    if (inside)
+        streamn_run<T, ORDER, RB, NS, FMA, false>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
+                                                  xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+    else
+        streamn_run<T, ORDER, RB, NS, FMA, true>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
+                                                 xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+}
+
 // ---------------------------------------------------------------- launchers
 struct Region {
     int xb, xe, yb, ye;
@@ -450,6 +651,61 @@ int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region
     CME_LAUNCH_STATUS();
 }
 
+// NS-step pass (NS = 3, 4; fp32): rows per block and chunk heights from
+// benchmarks/tune_heatn.py (profiles/heat_streamn_tune.md: at 16384^2 NS=3
+// RB=4 ~190-row chunks 0.178 ms/step, NS=4 RB=2 0.195, stream2 0.237).
+// CME_STREAMN_CHUNK overrides for experiments. Thin regions use the stream2
+// rule (about 1024 waves, latency-bound border strips).
+template <int NS, int RB>
+int streamn_chunk(int strips, int H, int chunk_hint) {
+    static const int env_chunk = [] {
+        const char* e = getenv("CME_STREAMN_CHUNK");
+        return e ? atoi(e) : 0;
+    }();
+    int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
+    if (chunk <= 0) {
+        const long target_waves = 256L * 24;
+        long rows = ((long)strips * H + target_waves - 1) / target_waves;
+        const long lo = 8 * RB > 32 ? 8 * RB : 32;
+        if ((long)strips * cdiv(H, lo) < 1024) {
+            rows = ((long)strips * H + 1023) / 1024;
+            rows = rows < RB ? RB : rows;
+        } else {
+            rows = rows < lo ? lo : rows;
+        }
+        rows = rows > 1024 ? 1024 : rows;
+        chunk = (int)rows;
+    }
+    return ((chunk + RB - 1) / RB) * RB;
+}
+
+template <typename T, int ORDER, int NS, bool FMA, int RB = (NS == 3 ? 4 : 2), int WPE = 1>
+int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl,
+                         T ycfl, int chunk_hint, hipStream_t s) {
+    static_assert(NS >= 3 && NS <= 4, "streamN: 3 or 4 steps per pass");
+    if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
+    S2Regions R{};
+    int waves = 0;
+    for (int i = 0; i < n; ++i) {
+        const Region& g = gs[i];
+        const int H = g.ye - g.yb;
+        if (H <= 0 || g.xe <= g.xb) continue;
+        const int strips = (int)cdiv(g.xe - (g.xb & ~3), StripN<NS>::kOut);
+        const int chunk = streamn_chunk<NS, RB>(strips, H, chunk_hint);
+        const int k = R.n++;
+        R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
+        R.strips[k] = strips;
+        R.chunk[k] = chunk;
+        waves += strips * (int)cdiv(H, chunk);
+        R.wave_end[k] = waves;
+    }
+    if (R.n == 0) return 0;
+    hipLaunchKernelGGL((heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
+                       curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
+    CME_LAUNCH_STATUS();
+}
+
 template <typename T, int ORDER, bool FMA, int RB = (sizeof(T) == 4 ? (FMA ? 2 : 4) : (FMA ? 4 : 2)), int WPE = 1>
 int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g1, T xcfl, T ycfl, int chunk_hint,
                    hipStream_t s) {
@@ -478,6 +734,23 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         // TWO timesteps per launch (temporal blocking), step-1 region = output
         return variant == 4 ? launch_stream2<T, ORDER, false>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s)
                             : launch_stream2<T, ORDER, true>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s);
+    } else if (variant >= 7 && variant <= 10) {
+        // NS = 3 (variants 7, 8) or 4 (9, 10) timesteps per launch; fp32 only
+        // (fp64 windows would not fit two waves per SIMD)
+        if constexpr (sizeof(T) == 4) {
+            switch (variant) {
+                case 7: return launch_streamn_multi<T, ORDER, 3, false>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                        chunk_hint, s);
+                case 8: return launch_streamn_multi<T, ORDER, 3, true>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                       chunk_hint, s);
+                case 9: return launch_streamn_multi<T, ORDER, 4, false>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                        chunk_hint, s);
+                default: return launch_streamn_multi<T, ORDER, 4, true>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                        chunk_hint, s);
+            }
+        } else {
+            return (int)hipErrorInvalidValue;
+        }
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -566,8 +839,57 @@ CME_EXPORT int cme_heat_step2_f64(const double* prev, double* curr, int pitch, i
                                     xcfl, ycfl, chunk, fma, as_stream(stream));
 }
 
+// NS timesteps in one pass (NS = 2, 3, 4; 3 and 4 fp32 only): intermediate
+// steps over `ext` (out grown by <= (NS-1)B cells into an NS*B-deep halo),
+// the last one writes `out` (nout <= 4 regions, one launch).
+namespace {
+template <int ORDER, bool FMA>
+int stepn_f32(const float* prev, float* curr, int pitch, int gy, const Region* gs, int n, Region e, int ns,
+              float xcfl, float ycfl, int chunk, hipStream_t s) {
+    switch (ns) {
+        case 2: return launch_stream2_multi<float, ORDER, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk, s);
+        case 3: return launch_streamn_multi<float, ORDER, 3, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk,
+                                                                  s);
+        case 4: return launch_streamn_multi<float, ORDER, 4, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk,
+                                                                  s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+template <bool FMA>
+int stepn_f32_o(int order, const float* prev, float* curr, int pitch, int gy, const Region* gs, int n, Region e,
+                int ns, float xcfl, float ycfl, int chunk, hipStream_t s) {
+    switch (order) {
+        case 2: return stepn_f32<2, FMA>(prev, curr, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 4: return stepn_f32<4, FMA>(prev, curr, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 8: return stepn_f32<8, FMA>(prev, curr, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_stepn_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
+                                  void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    return fma ? stepn_f32_o<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, chunk,
+                                   as_stream(stream))
+               : stepn_f32_o<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, chunk,
+                                    as_stream(stream));
+}
+
+CME_EXPORT int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                  const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
+                                  void* stream) {
+    if (nsteps != 2) return (int)hipErrorInvalidValue;  // deeper passes: fp32 only
+    return cme_heat_step2_f64(prev, curr, pitch, gy, out, nout, ext, order, xcfl, ycfl, chunk, fma, stream);
+}
+
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO
-// steps), 5 stream2 FMA (TWO steps), 6 stream FMA
+// steps), 5 stream2 FMA (TWO steps), 6 stream FMA, 7 / 8 stream3 exact / FMA
+// (THREE steps, fp32), 9 / 10 stream4 exact / FMA (FOUR steps, fp32)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -592,6 +914,17 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int cur = 0;
     T* bufs[2] = {a, b};
     int i = 0;
+    if (variant >= 7 && variant <= 10) {
+        if (sizeof(T) != 4) return (int)hipErrorInvalidValue;
+        const int ns = variant <= 8 ? 3 : 4;
+        for (; i + ns <= iters; i += ns) {
+            int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
+            if (rc) return rc;
+            cur ^= 1;
+        }
+        // remainder: two-step passes, then one single step
+        variant = (variant & 1) ? 4 : 5;
+    }
     if (variant == 4 || variant == 5) {
         for (; i + 1 < iters; i += 2) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
@@ -717,6 +1050,35 @@ CME_EXPORT int cme_heat_stream2_tune(const void* prev, void* curr, int dtype, in
                : tune2_rb<double, false>(p, c, pitch, gy, g, xcfl, ycfl, chunk, rb, wpe, s);
 }
 
+// Tuning entry for the NS-step kernels (order 8, fp32): ns 3/4, rows per
+// block rb 1/2/4, exact or FMA, explicit chunk (0 = default rule).
+namespace {
+template <int NS, bool FMA>
+int tunen_rb(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int rb,
+             hipStream_t s) {
+    switch (rb) {
+        case 1: return launch_streamn_multi<float, 8, NS, FMA, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        case 2: return launch_streamn_multi<float, 8, NS, FMA, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        case 4: return launch_streamn_multi<float, 8, NS, FMA, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_streamn_tune(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb,
+                                     int ye, float xcfl, float ycfl, int chunk, int rb, int ns, int fma,
+                                     void* stream) {
+    hipStream_t s = as_stream(stream);
+    const Region g{xb, xe, yb, ye};
+    if (ns == 3)
+        return fma ? tunen_rb<3, true>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s)
+                   : tunen_rb<3, false>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s);
+    if (ns == 4)
+        return fma ? tunen_rb<4, true>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s)
+                   : tunen_rb<4, false>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s);
+    return (int)hipErrorInvalidValue;
+}
+
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(heat_naive_f32_o8, 256, heat_naive_kernel<float, 8>);
 CME_REGISTER_KERNEL(heat_lds_f32_o8, 256, heat_lds_kernel<float, 8, 32, 1>);
@@ -724,3 +1086,5 @@ CME_REGISTER_KERNEL(heat_stream_f32_o8, 256, heat_stream_kernel<float, 8, 4>);
 CME_REGISTER_KERNEL(heat_stream2_f32_o8, 256, heat_stream2_kernel<float, 8, 4, false>);
 CME_REGISTER_KERNEL(heat_stream2_fma_f32_o8, 256, heat_stream2_kernel<float, 8, 4, true>);
 CME_REGISTER_KERNEL(heat_stream2_f64_o8, 256, heat_stream2_kernel<double, 8, 2, false>);
+CME_REGISTER_KERNEL(heat_stream3_fma_f32_o8, 256, heat_streamn_kernel<float, 8, 4, 3, true>);
+CME_REGISTER_KERNEL(heat_stream4_fma_f32_o8, 256, heat_streamn_kernel<float, 8, 2, 4, true>);

@@ -13,7 +13,7 @@ def _heat_rank(rank, world, method, sync, order, tblock=1, fma=False):
     from cme213x.parallel.comm import TorchComm
     from cme213x.utils.params import SimParams
 
-    p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
+    p = SimParams(nx=70, ny=104, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   sync=sync, flavor="hw5")
     sim = DistHeat(p, TorchComm(), torch.float64, "cpu", variant="naive", tblock=tblock, fma=fma)
     # non-uniform initial condition (same on every rank, by global coords)
@@ -35,7 +35,7 @@ def _single(method, order, sync, fma=False):
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.utils.params import SimParams
 
-    p = SimParams(nx=70, ny=52, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
+    p = SimParams(nx=70, ny=104, iters=9, order=order, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   sync=sync, flavor="hw5")
     sim = DistHeat(p, None, torch.float64, "cpu", variant="naive", fma=fma)
     g = sim.subs[0].grid
@@ -49,7 +49,8 @@ def _single(method, order, sync, fma=False):
 @pytest.mark.parametrize("method,sync,order,world,tblock",
                          [(1, True, 8, 2, 1), (1, False, 4, 2, 1), (2, False, 8, 4, 1), (2, True, 2, 4, 1),
                           (1, False, 8, 3, 2), (1, True, 4, 2, 2), (2, False, 8, 4, 2), (2, True, 2, 4, 2),
-                          (2, False, 4, 6, 2)])
+                          (2, False, 4, 6, 2), (1, False, 8, 3, 3), (2, True, 4, 4, 3), (1, False, 8, 2, 4),
+                          (2, False, 2, 4, 4)])
 @pytest.mark.parametrize("fma", [False, True])
 def test_dist_heat_matches_single(method, sync, order, world, tblock, fma):
     parts = run_ranks(_heat_rank, world, (method, sync, order, tblock, fma))
@@ -276,6 +277,6 @@ def _ckpt_rank(rank, world, directory, tblock):
     return bool(np.array_equal(a.state()[B:-B, B:-B], b.state()[B:-B, B:-B]))
 
 
-@pytest.mark.parametrize("tblock", [1, 2])
+@pytest.mark.parametrize("tblock", [1, 2, 4])
 def test_dist_heat_checkpoint_restart_gloo(tmp_path, tblock):
     assert all(run_ranks(_ckpt_rank, 4, (str(tmp_path), tblock)))

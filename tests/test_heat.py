@@ -186,6 +186,68 @@ def test_gpu_stream2_subregion(gpu, region, chunk, fma):
     assert torch.equal(oc, og.cpu())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("iters", [1, 4, 7, 9])
+def test_gpu_streamn_temporal_blocking_bitwise(gpu, order, ns, fma, iters):
+    # 3 / 4 steps per HBM pass (+ two-step and single-step tails) must equal
+    # single steps bit for bit, exact and FMA
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    c.run(iters, "fma" if fma else "naive")
+    g.run(iters, f"stream{ns}" + ("_fma" if fma else ""))
+    torch.cuda.synchronize()
+    d = ulp_distance(c.state(), g.state())
+    assert int(d.max()) == 0, f"max ulp {int(d.max())}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("region", [(4, 300, 4, 100), (9, 250, 17, 77), (130, 131, 5, 200), (8, 292, 8, 242)])
+@pytest.mark.parametrize("chunk", [0, 8, 14])
+@pytest.mark.parametrize("ns", [3, 4])
+def test_gpu_streamn_subregion(gpu, region, chunk, ns):
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    ca, cb = c.buf[0].clone(), c.buf[0].clone()
+    ga, gb = g.buf[0].clone(), g.buf[0].clone()
+    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 2 * ns, "fma")
+    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 2 * ns, f"stream{ns}_fma", chunk)
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns", [2, 3, 4])
+def test_gpu_stepn_multi_region_ext(gpu, ns):
+    """heat_stepn with several output regions in one launch and an
+    intermediate region grown past the output (the distributed border-strip
+    pass) equals the CPU composition of single steps."""
+    from cme213x.ops.stencil import heat_stepn
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    regs = [(4, 304, 4, 40), (4, 304, 220, 254), (4, 40, 40, 220), (270, 304, 40, 220)]
+    ext = (4, 304, 4, 254)
+    oc, og = c.buf[0].clone(), g.buf[0].clone()
+    heat_stepn(c.buf[0], oc, regs, ext, 8, c.xcfl, c.ycfl, ns, fma=True)
+    heat_stepn(g.buf[0], og, regs, ext, 8, g.xcfl, g.ycfl, ns, fma=True)
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+
+
+def test_streamn_is_fp32_only():
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=40, ny=30, order=2)
+    c = _rand_grid(p, torch.float64)
+    with pytest.raises(ValueError):
+        heat_run(c.buf[0], c.buf[1], c.interior, 2, c.xcfl, c.ycfl, 4, "stream4")
+
+
 def test_stream2_rejected_for_single_step():
     p = SimParams(nx=40, ny=30, order=2)
     c = _rand_grid(p, torch.float32)
