@@ -69,6 +69,9 @@ def _load(kind: str) -> ctypes.CDLL:
         if kind in _libs:
             return _libs[kind]
         path = _LIB_DIR / f"libcme213_{kind}.so"
+        alt = os.environ.get(f"CME_{kind.upper()}_LIB")  # experiments: an alternative build of the library
+        if alt:
+            path = Path(alt)
         if not path.exists():
             if os.environ.get("CME_AUTOBUILD", "1") != "0":
                 from . import _build

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Compute side of the strong-scaling flagship on ONE GPU: time one rank's
-per-step schedule (deep interior + border strips, two fused steps per pass)
+per-step schedule (deep interior + border strips, tblock fused steps per pass)
 for the subdomain an N-GPU run gives each rank, with the halo exchange
 replaced by a no-op. ms/step x N vs the N=1 time shows how much of ideal
 strong scaling the compute schedule itself keeps (launch overhead, thin
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--fma", type=int, default=1)
+    ap.add_argument("--tblock", type=int, default=3, help="timesteps per exchange / HBM pass (1-4)")
     ap.add_argument("--native", type=int, default=1, help="1: native loop (null transport); 0: Python loop")
     args = ap.parse_args()
     import torch
@@ -51,7 +52,7 @@ def main():
     for w in args.world:
         rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
         p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=False, flavor="hw5")
-        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=2, fma=bool(args.fma))
+        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=bool(args.fma))
 
         def run(k):
             if args.native:
@@ -68,7 +69,7 @@ def main():
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.steps
         base = base or ms * w
-        print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native,
+        print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
                           "ms_per_step": round(ms, 4),
                           "compute_scaling_eff": round(base / (ms * w), 3)}), flush=True)
         del sim

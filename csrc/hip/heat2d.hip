@@ -406,14 +406,15 @@ struct StripN {
     static constexpr int kOut = (64 - 2 * NS) * 4;
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK>
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD = 1>
 struct StreamN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
-    static constexpr int P = NW / cgcd(NW, RB);
+    static constexpr int P = NW / cgcd(NW, RB);  // phases until the window rings realign
+    static constexpr int Q = P * PD / cgcd(P, PD);  // ... and the PD prefetch buffers
 
     V4<T> w[NS][NW];
-    V4<T> nxt[RB];
+    V4<T> nxt[PD][RB];  // input rows of the next PD phases, in flight
     const T* src;
     T* dst;
     int pitch, gy, xbase;
@@ -481,11 +482,12 @@ struct StreamN {
     __device__ __forceinline__ bool phase() {
         if (r0 - (NS - 1) * B >= y1) return false;
         constexpr int S = (PH * RB) % NW;
+        constexpr int F = PH % PD;
 #pragma unroll
-        for (int i = 0; i < RB; ++i) w[0][(S + 2 * B + i) % NW] = nxt[i];
-        if (r0 + RB < y1 + (NS - 1) * B) {
+        for (int i = 0; i < RB; ++i) w[0][(S + 2 * B + i) % NW] = nxt[F][i];
+        if (r0 + PD * RB < y1 + (NS - 1) * B) {
 #pragma unroll
-            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
+            for (int i = 0; i < RB; ++i) nxt[F][i] = load4(row_ptr(r0 + PD * RB + B + i));
         }
         inter<1, S>();
 #pragma unroll
@@ -508,7 +510,7 @@ struct StreamN {
             }
         }
         r0 += RB;
-        if constexpr (PH + 1 < P)
+        if constexpr (PH + 1 < Q)
             return phase<PH + 1>();
         else
             return true;
@@ -519,17 +521,19 @@ struct StreamN {
 #pragma unroll
         for (int i = 0; i < 2 * B; ++i) w[0][i] = load4(row_ptr(r0 - B + i));
 #pragma unroll
-        for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + B + i));
+        for (int f = 0; f < PD; ++f)
+#pragma unroll
+            for (int i = 0; i < RB; ++i) nxt[f][i] = load4(row_ptr(r0 + f * RB + B + i));
         while (phase<0>()) {
         }
     }
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK>
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD>
 __device__ __forceinline__ void streamn_run(const T* src, T* dst, int pitch, int gy, int xbase, bool out_lane,
                                             bool full_vec, int y0, int y1, int xb, int xe, int xb1, int xe1, int yb1,
                                             int ye1, T xcfl, T ycfl) {
-    StreamN<T, ORDER, RB, NS, FMA, CHECK> st;
+    StreamN<T, ORDER, RB, NS, FMA, CHECK, PD> st;
     st.src = src;
     st.dst = dst;
     st.pitch = pitch;
@@ -550,7 +554,7 @@ __device__ __forceinline__ void streamn_run(const T* src, T* dst, int pitch, int
     st.run();
 }
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, int WPE = 1>
+template <typename T, int ORDER, int RB, int NS, bool FMA, int WPE = 1, int PD = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_streamn_kernel(
     const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
     int ye1, T xcfl, T ycfl) {
@@ -579,10 +583,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
                         (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
     if (inside)
-        streamn_run<T, ORDER, RB, NS, FMA, false>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
+        streamn_run<T, ORDER, RB, NS, FMA, false, PD>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
                                                   xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
     else
-        streamn_run<T, ORDER, RB, NS, FMA, true>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
+        streamn_run<T, ORDER, RB, NS, FMA, true, PD>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
                                                  xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
 }
 
@@ -679,7 +683,7 @@ int streamn_chunk(int strips, int H, int chunk_hint) {
     return ((chunk + RB - 1) / RB) * RB;
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int RB = (NS == 3 ? 4 : 2), int WPE = 1>
+template <typename T, int ORDER, int NS, bool FMA, int RB = (NS == 3 ? 4 : 2), int WPE = 1, int PD = 1>
 int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl,
                          T ycfl, int chunk_hint, hipStream_t s) {
     static_assert(NS >= 3 && NS <= 4, "streamN: 3 or 4 steps per pass");
@@ -701,7 +705,7 @@ int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region
         R.wave_end[k] = waves;
     }
     if (R.n == 0) return 0;
-    hipLaunchKernelGGL((heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
+    hipLaunchKernelGGL((heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
                        curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
     CME_LAUNCH_STATUS();
 }
@@ -1050,32 +1054,38 @@ CME_EXPORT int cme_heat_stream2_tune(const void* prev, void* curr, int dtype, in
                : tune2_rb<double, false>(p, c, pitch, gy, g, xcfl, ycfl, chunk, rb, wpe, s);
 }
 
-// Tuning entry for the NS-step kernels (order 8, fp32): ns 3/4, rows per
-// block rb 1/2/4, exact or FMA, explicit chunk (0 = default rule).
+// Tuning entry for the NS-step kernels (order 8, fp32, FMA): ns 3/4, rows per
+// block rb 1/2/4, prefetch depth pd 1/2 (phases of input rows in flight),
+// explicit chunk (0 = default rule).
 namespace {
-template <int NS, bool FMA>
-int tunen_rb(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int rb,
+template <int NS, int RB>
+int tunen_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int pd,
              hipStream_t s) {
+    switch (pd) {
+        case 1: return launch_streamn_multi<float, 8, NS, true, RB, 1, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        case 2: return launch_streamn_multi<float, 8, NS, true, RB, 1, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+template <int NS>
+int tunen_rb(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int rb,
+             int pd, hipStream_t s) {
     switch (rb) {
-        case 1: return launch_streamn_multi<float, 8, NS, FMA, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
-        case 2: return launch_streamn_multi<float, 8, NS, FMA, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
-        case 4: return launch_streamn_multi<float, 8, NS, FMA, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        case 1: return tunen_pd<NS, 1>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, s);
+        case 2: return tunen_pd<NS, 2>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, s);
+        case 4: return tunen_pd<NS, 4>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
 }  // namespace
 
 CME_EXPORT int cme_heat_streamn_tune(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb,
-                                     int ye, float xcfl, float ycfl, int chunk, int rb, int ns, int fma,
+                                     int ye, float xcfl, float ycfl, int chunk, int rb, int ns, int pd,
                                      void* stream) {
     hipStream_t s = as_stream(stream);
     const Region g{xb, xe, yb, ye};
-    if (ns == 3)
-        return fma ? tunen_rb<3, true>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s)
-                   : tunen_rb<3, false>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s);
-    if (ns == 4)
-        return fma ? tunen_rb<4, true>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s)
-                   : tunen_rb<4, false>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, s);
+    if (ns == 3) return tunen_rb<3>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, s);
+    if (ns == 4) return tunen_rb<4>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, s);
     return (int)hipErrorInvalidValue;
 }
 
