@@ -1055,8 +1055,8 @@ CME_EXPORT int cme_heat_stream2_tune(const void* prev, void* curr, int dtype, in
 }
 
 // Tuning entry for the NS-step kernels (order 8, fp32, FMA): ns 3/4, rows per
-// block rb 1/2/4, prefetch depth pd 1/2 (phases of input rows in flight),
-// explicit chunk (0 = default rule).
+// block rb 1/2/4, prefetch depth pd 1/2 (phases of input rows in flight; 13 =
+// depth 1 under a 3-waves/SIMD register cap), explicit chunk (0 = default).
 namespace {
 template <int NS, int RB>
 int tunen_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int pd,
@@ -1064,6 +1064,8 @@ int tunen_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
     switch (pd) {
         case 1: return launch_streamn_multi<float, 8, NS, true, RB, 1, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
         case 2: return launch_streamn_multi<float, 8, NS, true, RB, 1, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        // pd 13: prefetch depth 1 with a 3-waves-per-SIMD register cap (<= 168 VGPRs)
+        case 13: return launch_streamn_multi<float, 8, NS, true, RB, 3, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
