@@ -85,6 +85,8 @@ def _load(kind: str) -> ctypes.CDLL:
         if kind == "hip":
             lib.cme_hip_error_string.restype = ctypes.c_char_p
             lib.cme_hip_error_string.argtypes = [ctypes.c_int]
+            lib.cme_rccl_error_string.restype = ctypes.c_char_p
+            lib.cme_rccl_error_string.argtypes = [ctypes.c_int]
         _libs[kind] = lib
         return lib
 
@@ -104,6 +106,9 @@ def hip_loaded() -> bool:
 def check(rc: int, what: str, kind: str = "hip") -> None:
     if rc != 0:
         if kind == "hip":
+            if rc >= 10000:  # 10000 + ncclResult_t (NCCL_TRY in csrc/hip/dist_heat.hip)
+                msg = hip().cme_rccl_error_string(int(rc)).decode()
+                raise RuntimeError(f"{what}: RCCL error {rc - 10000} ({msg})")
             msg = hip().cme_hip_error_string(int(rc)).decode()
             raise RuntimeError(f"{what}: HIP error {rc} ({msg})")
         raise RuntimeError(f"{what}: native CPU backend returned {rc}")

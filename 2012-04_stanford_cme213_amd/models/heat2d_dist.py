@@ -48,7 +48,24 @@ class SubDesc(ctypes.Structure):
                 ("interior", ctypes.c_void_p), ("n_int", ctypes.c_int), ("border", ctypes.c_void_p),
                 ("n_b", ctypes.c_int), ("ext", ctypes.c_void_p), ("rows", ctypes.c_void_p),
                 ("n_rows", ctypes.c_int), ("blks", ctypes.c_void_p), ("n_blks", ctypes.c_int),
-                ("stage", ctypes.c_void_p), ("rank", ctypes.c_int)]
+                ("stage", ctypes.c_void_p), ("rank", ctypes.c_int), ("ipc", ctypes.c_void_p)]
+
+
+class IpcPeerDesc(ctypes.Structure):
+    """Mirror of ``IpcPeerDesc`` (``csrc/hip/dist_heat.hip``): one
+    neighbouring process's mapped memory."""
+    _fields_ = [("buf", ctypes.c_void_p * 2), ("stage", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("rank", ctypes.c_int), ("slot", ctypes.c_int)]
+
+
+class IpcPlan(ctypes.Structure):
+    """Mirror of ``IpcPlan``: transport 3 of the native loop."""
+    _fields_ = [("flags", ctypes.c_void_p), ("timeout", ctypes.c_void_p), ("epoch", ctypes.c_void_p),
+                ("row_src", ctypes.c_void_p), ("blk_src", ctypes.c_void_p), ("npeer", ctypes.c_int),
+                ("peer", IpcPeerDesc * 8)]
+
+
+_IPC_TIMEOUT_WORD = 16  # index of the give-up word in the flags tensor
 
 
 class _Sub:
@@ -329,10 +346,80 @@ class DistHeat:
             d.blks, d.n_blks = pl["cols"].data_ptr(), pl["cols"].shape[0]
             d.stage = pl["stage"].data_ptr()
             d.rank = r
+            d.ipc = None
         self._plan = {"subs": arr, "plans": plans}
         return self._plan
 
-    def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None) -> None:
+    def _ipc_plan(self, ipc):
+        """Build (once per :class:`~cme213x.parallel.ipc.NativeIpc`) the
+        transport-3 plan of this process's subdomain: export its grid, staging
+        and epoch words, all-gather every rank's descriptors and exchange plan,
+        map the neighbours' memory and find, for each halo piece, where the
+        neighbour keeps the data destined to us. Collective over ipc's group."""
+        st = getattr(self, "_ipc", None)
+        if st is not None and st["ipc"] is ipc:
+            return st
+        if len(self.subs) != 1:
+            raise ValueError("IPC transport: one subdomain per process")
+        (r, s), = self.subs.items()
+        pl = self._native_plan()["plans"][r]
+        g = s.grid
+        flags = torch.zeros(32, dtype=torch.int32, device=g.device)
+        rows = [list(map(int, x)) for x in pl["rows"].tolist()]
+        cols = [list(map(int, x)) for x in pl["cols"].tolist()]
+        neigh = sorted({x[0] for x in rows} | {c[0] for c in cols})
+        if len(neigh) > 8:
+            raise ValueError("IPC transport: at most 8 neighbours")
+        info = {"rank": r, "buf": ipc.export(g.buf), "stage": ipc.export(pl["stage"]), "flags": ipc.export(flags),
+                "state_bytes": g.buf[0].numel() * g.buf.element_size(), "rows": rows, "cols": cols, "neigh": neigh}
+        torch.cuda.synchronize(g.device)  # epoch words are zero before any peer can map them
+        by_rank = {i["rank"]: i for i in ipc.allgather_object(info)}
+        plan = IpcPlan()
+        plan.npeer = len(neigh)
+        for j, p in enumerate(neigh):
+            pi = by_rank[p]
+            d = plan.peer[j]
+            b0 = ipc.open(*pi["buf"])
+            d.buf[0], d.buf[1] = b0, b0 + pi["state_bytes"]
+            d.stage = ipc.open(*pi["stage"])
+            d.flags = ipc.open(*pi["flags"])
+            d.rank, d.slot = p, pi["neigh"].index(r)
+        row_src = (ctypes.c_longlong * max(1, len(rows)))()
+        for i, x in enumerate(rows):
+            mine = [y for y in by_rank[x[0]]["rows"] if y[0] == r]
+            if len(mine) != 1 or mine[0][3] != x[3]:
+                raise RuntimeError(f"rank {r}: inconsistent row halo plan with rank {x[0]}")
+            row_src[i] = mine[0][1]
+        blk_src = (ctypes.c_longlong * max(1, len(cols)))()
+        for i, c in enumerate(cols):
+            pc = by_rank[c[0]]["cols"]
+            m = [k for k, y in enumerate(pc) if y[0] == r]
+            if len(m) != 1 or pc[m[0]][5:7] != c[5:7]:
+                raise RuntimeError(f"rank {r}: inconsistent block halo plan with rank {c[0]}")
+            blk_src[i] = sum(y[5] * y[6] for y in pc[:m[0]])
+        epoch = ctypes.c_longlong(0)
+        plan.flags = flags.data_ptr()
+        plan.timeout = flags.data_ptr() + 4 * _IPC_TIMEOUT_WORD
+        plan.epoch = ctypes.addressof(epoch)
+        plan.row_src, plan.blk_src = ctypes.addressof(row_src), ctypes.addressof(blk_src)
+        st = {"ipc": ipc, "plan": plan, "flags": flags, "epoch": epoch, "row_src": row_src, "blk_src": blk_src}
+        ipc.keep(flags, pl["stage"], g.buf)
+        self._ipc = st
+        return st
+
+    def ipc_check(self) -> None:
+        """Raise if a wait of the IPC transport gave up on a peer (a peer that
+        died or never signalled: the kernels stop waiting instead of hanging
+        the GPU, and the state is then invalid)."""
+        st = getattr(self, "_ipc", None)
+        if st is None:
+            return
+        torch.cuda.synchronize(st["flags"].device)
+        if int(st["flags"][_IPC_TIMEOUT_WORD].item()) != 0:
+            raise RuntimeError("IPC halo exchange timed out waiting for a peer; state is invalid")
+
+    def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None,
+                   ipc=None) -> None:
         """``iters`` timesteps in ONE native call (``cme_heat_dist_run``):
         border strips on their own stream, the halo exchange posted as soon
         as they finish, the deep interior overlapping both; with ``tblock=n``
@@ -348,13 +435,16 @@ class DistHeat:
 
         if rccl is not None and len(self.subs) != 1:
             raise ValueError("RCCL transport: one subdomain per process")
+        if rccl is not None and ipc is not None:
+            raise ValueError("choose one transport: rccl or ipc")
         self.finish()
         sync = self.p.sync if sync is None else sync
         plan = self._native_plan()
         g0 = next(iter(self.subs.values())).grid
         cur_out = ctypes.c_int(0)
         if transport is None:
-            transport = 0 if rccl is not None else 1
+            transport = 0 if rccl is not None else (3 if ipc is not None else 1)
+        plan["subs"][0].ipc = ctypes.addressof(self._ipc_plan(ipc)["plan"]) if transport == 3 else None
         _ext.call_hip("cme_heat_dist_run", transport, rccl.handle if rccl is not None else None,
                       ctypes.addressof(plan["subs"]), len(self.subs), 0 if g0.dtype == torch.float32 else 1,
                       g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock, int(self.fma),
@@ -431,7 +521,8 @@ class DistHeat:
         if len(its) != 1:
             raise ValueError("subdomain checkpoints from different iterations")
         self.iteration = its.pop()
-        self._plan = None
+        # the native / IPC plans depend on geometry only: kept (peers' IPC
+        # mappings of our grid and staging stay valid)
         self.exchange(self._cur()).wait()
 
     # -- io ------------------------------------------------------------------

@@ -81,11 +81,43 @@ class TorchComm(Comm):
     def exchange(self, ops: list[P2P]) -> Pending:
         if not ops:
             return Pending()
+        if self.backend == "gloo" and any(o.tensor.is_cuda for o in ops):
+            return self._exchange_host_staged(ops)
         p2p = [dist.P2POp(dist.isend if o.kind == "send" else dist.irecv, o.tensor, self._global(o.peer),
                           group=self.group) for o in ops]
         return Pending(dist.batch_isend_irecv(p2p))
 
+    def _exchange_host_staged(self, ops: list[P2P]) -> Pending:
+        """gloo moves host memory only: device tensors are staged through
+        host copies (control-plane use, e.g. the initial halo fill of ranks
+        whose data plane is :class:`~cme213x.parallel.ipc.NativeIpc`)."""
+        host, back = [], []
+        for o in ops:
+            if o.kind == "send":
+                host.append(o.tensor.detach().to("cpu", copy=True).contiguous())
+            else:
+                h = torch.empty(o.tensor.shape, dtype=o.tensor.dtype)
+                host.append(h)
+                back.append((o.tensor, h))
+        p2p = [dist.P2POp(dist.isend if o.kind == "send" else dist.irecv, h, self._global(o.peer),
+                          group=self.group) for o, h in zip(ops, host)]
+        works = dist.batch_isend_irecv(p2p)
+
+        class _Staged(Pending):
+            def wait(self_inner):
+                for w in works:
+                    w.wait()
+                for dst, h in back:
+                    dst.copy_(h)
+
+        return _Staged()
+
     def allreduce_(self, t, op="sum"):
+        if self.backend == "gloo" and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, _OPS[op], group=self.group)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, _OPS[op], group=self.group)
         return t
 
@@ -106,6 +138,11 @@ class TorchComm(Comm):
         return out
 
     def broadcast_(self, t, src=0):
+        if self.backend == "gloo" and t.is_cuda:
+            h = t.cpu()
+            dist.broadcast(h, self._global(src), group=self.group)
+            t.copy_(h)
+            return t
         dist.broadcast(t, self._global(src), group=self.group)
         return t
 

@@ -35,11 +35,27 @@ sys.path.insert(0, REPO)
 BASELINE_GBPS = 239.7  # heat 4000^2 order 8 LDS kernel, 48.07 ms / 10 iters, 72 B/pt
 
 
-def native_selftest(comm, rccl, dev, args) -> bool:
-    """Run a small problem through the native RCCL loop AND the
-    torch.distributed loop (the path the multi-process CPU tests cover) and
-    require bitwise-equal subdomains on every rank before trusting the native
-    loop for the measurement."""
+def _wait_bounded(dev, seconds: float) -> bool:
+    """Wait for the work queued on the current stream, giving up after
+    ``seconds`` (a hung exchange must not hang the bench)."""
+    import torch
+
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    t_end = time.perf_counter() + seconds
+    while not ev.query():
+        if time.perf_counter() > t_end:
+            return False
+        time.sleep(0.005)
+    return True
+
+
+def native_selftest(comm, native, dev, args) -> bool:
+    """Run a small problem through the native loop (RCCL or IPC transport)
+    AND the torch.distributed loop (the path the multi-process CPU tests
+    cover) and require bitwise-equal subdomains on every rank before trusting
+    the native loop for the measurement. A native run that does not finish
+    within 60 s counts as a failure (the caller aborts the communicator)."""
     import torch
 
     from cme213x.models.heat2d_dist import DistHeat
@@ -57,7 +73,14 @@ def native_selftest(comm, rccl, dev, args) -> bool:
         xx = torch.arange(s.blk.nx, device=dev, dtype=torch.float32).view(1, -1) + s.blk.x0
         g.buf[:, B:B + s.blk.ny, B:B + s.blk.nx] = 5.0 + torch.sin(0.05 * xx) * torch.cos(0.03 * yy)
         sim.exchange(sim._cur()).wait()
-    a.run_native(6, rccl)
+    if args.transport == "ipc":
+        a.run_native(6, ipc=native)
+    else:
+        a.run_native(6, native)
+    if not _wait_bounded(dev, 60.0):
+        raise TimeoutError("native loop self-test did not finish within 60 s")
+    if args.transport == "ipc":
+        a.ipc_check()
     for _ in range(6):
         b.step()
     b.finish()
@@ -89,7 +112,11 @@ def main() -> int:
     ap.add_argument("--tblock", type=int, choices=[1, 2, 3, 4], default=3,
                     help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
-                    help="multi-GPU: run the K-step loop in C++ over a native RCCL communicator")
+                    help="multi-GPU: run the K-step loop in C++ over a native communicator (auto: after a "
+                         "bitwise self-test against the torch.distributed loop)")
+    ap.add_argument("--transport", choices=["rccl", "ipc"], default="rccl",
+                    help="native halo transport: rccl = grouped ncclSend/Recv; ipc = peers' memory mapped "
+                         "with hipIpcOpenMemHandle, pulled by a kernel over xGMI")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
                          "(tests; never the reported number)")
@@ -106,10 +133,9 @@ def main() -> int:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        if args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch under torch.distributed.run",
-                  file=sys.stderr)
-            return 2
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU under "
+              "torch.distributed.run with --nproc-per-node equal to --gpus", file=sys.stderr)
+        return 2
     on_gpu = args.device == "cuda"
     comm = init_from_env(args.device)
     rank = comm.rank
@@ -122,34 +148,57 @@ def main() -> int:
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
-    rccl, native_ok = None, False
-    if on_gpu and comm.size > 1 and args.native != "off":
-        from cme213x.parallel.rccl import NativeRccl
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1.0 if ok else 0.0], device=dev)
+        comm.allreduce_(t, "min")
+        return bool(t.item() == 1.0)
 
-        # any failure on any rank (communicator setup or the self-test) makes
-        # every rank fall back to the torch.distributed loop together
+    native, native_ok = None, False
+    if on_gpu and comm.size > 1 and args.native != "off":
+        # 1) every rank can load the native library -- agreed BEFORE any
+        #    collective native setup, so no rank is left alone inside
+        #    ncclCommInitRank / the IPC handle exchange
         try:
-            rccl = NativeRccl()
-            native_ok = native_selftest(comm, rccl, dev, args) if args.native == "auto" else True
-        except Exception as e:  # noqa: BLE001 - reported, then the portable path runs
-            print(f"bench.py rank {rank}: native RCCL loop unavailable ({e}); using torch.distributed",
-                  file=sys.stderr)
-            native_ok = False
-        agree = torch.tensor([1.0 if native_ok else 0.0], device=dev)
-        comm.allreduce_(agree, "min")
-        native_ok = bool(agree.item() == 1.0)
+            cme213x._ext.hip()
+            lib_ok = True
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py rank {rank}: native library unavailable ({e})", file=sys.stderr)
+            lib_ok = False
+        native_ok = agree(lib_ok)
+        # 2) collective setup + bitwise self-test; any failure (or a hang,
+        #    bounded at 60 s) on any rank makes every rank fall back together
+        if native_ok:
+            try:
+                if args.transport == "ipc":
+                    from cme213x.parallel.ipc import NativeIpc
+
+                    native = NativeIpc()
+                else:
+                    from cme213x.parallel.rccl import NativeRccl
+
+                    native = NativeRccl()
+                native_ok = native_selftest(comm, native, dev, args) if args.native == "auto" else True
+            except Exception as e:  # noqa: BLE001 - reported, then the portable path runs
+                print(f"bench.py rank {rank}: native {args.transport} loop unavailable ({e}); "
+                      "using torch.distributed", file=sys.stderr)
+                native_ok = False
+                if native is not None and args.transport == "rccl":
+                    native.abort()  # pending native sends/recvs fail on the peers instead of hanging
+            native_ok = agree(native_ok)
         if not native_ok and args.native == "on":
             print("bench.py: --native on but the native loop failed", file=sys.stderr)
             return 3
-    use_native = rccl is not None and native_ok
+    use_native = native is not None and native_ok
 
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
                    fma=bool(args.fma))
     init_state = {(s.blk.x0, s.blk.y0): s.grid.buf.clone() for s in sim.subs.values()} if on_gpu else {}
 
     def run(k):
-        if use_native:
-            sim.run_native(k, rccl)
+        if use_native and args.transport == "ipc":
+            sim.run_native(k, ipc=native)
+        elif use_native:
+            sim.run_native(k, native)
         else:
             sim.run(k)
 
@@ -182,8 +231,10 @@ def main() -> int:
     sync()
     t1 = time.perf_counter()
     comm.barrier()
-    if rccl is not None:
-        rccl.check()  # surface asynchronous RCCL failures instead of reporting a number
+    if use_native and args.transport == "rccl":
+        native.check()  # surface asynchronous RCCL failures instead of reporting a number
+    elif use_native:
+        sim.ipc_check()  # a wait that gave up on a peer invalidates the run
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     comm.allreduce_(elapsed, "max")
     secs = float(elapsed.item())
@@ -225,16 +276,19 @@ def main() -> int:
                 "fma": bool(args.fma),
                 "tblock": args.tblock,
                 "device": args.device,
-                "loop": "native-rccl" if use_native else ("torch.distributed" if comm.size > 1 else "single"),
+                "loop": f"native-{args.transport}" if use_native else ("torch.distributed" if comm.size > 1
+                                                                         else "single"),
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
             "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),
             "gpoints_per_s": round(pts * args.steps / secs / 1e9, 2),
             "sanity_ok": bool(bad.item() == 0),
-            "native_selftest": (native_ok if rccl is not None else None),
+            "native_selftest": (native_ok if native is not None else None),
             "spinup_steps": spin,
         }
         print(json.dumps(rec), flush=True)
+    if use_native and args.transport == "ipc":
+        native.close()
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

@@ -1,19 +1,40 @@
-// Native RCCL communicator + the distributed heat-stencil time loop.
+// Native communicators + the distributed heat-stencil time loop.
 //
 // Replaces the reference's host-MPI halo exchange (hw/hw5/2dHeat_solution.cpp:
 // 394-465, 501-628: MPI_Isend/Irecv per row -- or per grid ROW for column
-// halos -- then MPI_Waitall) with:
-//   * one ncclGroupStart/End batch of ncclSend/ncclRecv per exchange on a
-//     dedicated communication stream (rows go straight out of / into the grid;
-//     column halos are packed by a kernel into a contiguous staging buffer);
-//   * the deep-interior sweep of step t+1 running on the compute stream while
-//     the exchange of step t is in flight; the border strips wait on an event
-//     recorded after the exchange -- no host synchronisation in the loop;
-//   * the whole K-step loop issued from C++ (no per-step Python), RCCL
-//     bootstrapped from a unique id broadcast by torch.distributed.
+// halos -- then MPI_Waitall) with one exchange PLAN per subdomain and three
+// interchangeable transports that all execute it the same way:
+//
+//   pack   : the column / corner blocks this subdomain sends are gathered by
+//            ONE kernel into the send half of a contiguous staging buffer
+//            (rows are contiguous in the grid and travel straight from it);
+//   move   : 0 RCCL   -- one ncclGroupStart/End batch of ncclSend/ncclRecv;
+//            1 loopback -- every neighbour lives in this process: one
+//              multi-segment copy kernel PULLS the neighbours' rows (grid)
+//              and blocks (their staging) into our grid / staging;
+//            3 IPC    -- every neighbour is another process (same GPU or a
+//              peer over xGMI): its grid and staging are mapped with
+//              hipIpcOpenMemHandle and the same copy kernel pulls from them,
+//              ordered by epoch flags in peer-visible memory (below);
+//            2 none   -- no exchange (benchmarks the compute schedule);
+//   unpack : ONE kernel scatters the receive half of the staging into the
+//            ghost columns / corners.
+// So the loopback and IPC tests execute the exact pack / stage layout /
+// unpack code the RCCL transport runs -- only the "move" differs.
+//
+// Schedule (dist_run): the deep-interior sweep of pass i+1 runs on the compute
+// stream while the exchange of pass i is in flight on the comm stream; the
+// border strips wait on an event recorded after the exchange -- no host
+// synchronisation in the K-step loop, which is issued entirely from C++.
+//
 // torch is imported before this library is loaded, so librccl.so.1 resolves
 // to the RCCL instance torch already loaded (one RCCL per process).
 #include <rccl/rccl.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "cme213/common.h"
 
@@ -34,6 +55,8 @@ extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, i
         if (_ri) return _ri;              \
     } while (0)
 
+// RCCL status codes are returned as 10000 + ncclResult_t so the Python layer
+// can tell them from hipError_t (decoded with cme_rccl_error_string).
 #define NCCL_TRY(expr)                                        \
     do {                                                      \
         ncclResult_t _r = (expr);                             \
@@ -130,26 +153,193 @@ CME_EXPORT int cme_rccl_p2p(void* comm, int n, const int* peers, const int* is_s
     return 0;
 }
 
+// ------------------------------------------------------------ IPC memory
+// Export / import device allocations between processes (SURVEY §2.6
+// IpcPeerComm). Handles are always taken on the allocation BASE (found with
+// hipMemGetAddressRange), the interior offset travels separately, so a tensor
+// carved out of a caching-allocator segment maps correctly. Imports are
+// reference-counted per handle: a process maps each peer segment once even
+// when several tensors (grid, staging, flags) live in it.
 namespace {
+struct IpcImport {
+    void* base = nullptr;
+    int refs = 0;
+};
+std::mutex g_ipc_mu;
+std::map<std::string, IpcImport> g_ipc_imports;
+}  // namespace
 
-// Staged rectangular blocks (column halos, corner halos): rows x w elements
-// at (x0, y0) <-> contiguous staging.
-template <typename T>
-__global__ __launch_bounds__(256) void pack_block_kernel(const T* __restrict__ g, int pitch, int x0, int y0, int ny,
-                                                         int w, T* __restrict__ stage) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= ny * w) return;
-    const int r = i / w, c = i % w;
-    stage[i] = g[(size_t)(y0 + r) * pitch + x0 + c];
+CME_EXPORT int cme_ipc_export(const void* ptr, void* handle64, long long* offset) {
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    CME_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr));
+    hipIpcMemHandle_t h;
+    CME_TRY(hipIpcGetMemHandle(&h, (void*)base));
+    memcpy(handle64, &h, sizeof(h));
+    *offset = (long long)((const char*)ptr - (const char*)base);
+    return 0;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void unpack_block_kernel(T* __restrict__ g, int pitch, int x0, int y0, int ny, int w,
-                                                           const T* __restrict__ stage) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= ny * w) return;
-    const int r = i / w, c = i % w;
-    g[(size_t)(y0 + r) * pitch + x0 + c] = stage[i];
+CME_EXPORT int cme_ipc_open(const void* handle64, void** base) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    std::string key((const char*)handle64, sizeof(hipIpcMemHandle_t));
+    IpcImport& imp = g_ipc_imports[key];
+    if (imp.refs == 0) {
+        hipIpcMemHandle_t h;
+        memcpy(&h, handle64, sizeof(h));
+        void* p = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            g_ipc_imports.erase(key);
+            return (int)e;
+        }
+        imp.base = p;
+    }
+    ++imp.refs;
+    *base = imp.base;
+    return 0;
+}
+
+CME_EXPORT int cme_ipc_close(void* base) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto it = g_ipc_imports.begin(); it != g_ipc_imports.end(); ++it) {
+        if (it->second.base != base) continue;
+        if (--it->second.refs == 0) {
+            void* p = it->second.base;
+            g_ipc_imports.erase(it);
+            CME_TRY(hipIpcCloseMemHandle(p));
+        }
+        return 0;
+    }
+    return (int)hipErrorInvalidValue;
+}
+
+namespace {
+
+// ------------------------------------------------------------ exchange kernels
+constexpr int kMaxPieces = 8;  // column halos (2) + corner blocks (4) per subdomain
+constexpr int kMaxSegs = 16;   // rows (2) + blocks (6) per pull
+
+// A list of staged rectangular blocks: piece p is rows[p] x width[p]
+// elements at (x[p], y[p]) of the grid <-> stage + off[p].
+struct BlkList {
+    int x[kMaxPieces], y[kMaxPieces], rows[kMaxPieces], width[kMaxPieces];
+    long long off[kMaxPieces];
+    int n;
+};
+
+// One launch packs (grid -> stage) or unpacks (stage -> grid) every piece:
+// blockIdx.y = piece, grid-stride over its elements.
+template <typename T, bool kPack>
+__global__ __launch_bounds__(256) void blocks_kernel(T* __restrict__ g, int pitch, T* __restrict__ stage,
+                                                     BlkList l) {
+    const int p = blockIdx.y;
+    if (p >= l.n) return;
+    const int w = l.width[p], cnt = l.rows[p] * w;
+    T* st = stage + l.off[p];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += gridDim.x * 256) {
+        const int r = i / w, c = i - r * w;
+        T* gp = g + (size_t)(l.y[p] + r) * pitch + l.x[p] + c;
+        if (kPack)
+            st[i] = *gp;
+        else
+            *gp = st[i];
+    }
+}
+
+// Multi-segment device copy (the "move" of the loopback and IPC transports):
+// blockIdx.y = segment; 16-B lanes when the segment allows, 4-B otherwise
+// (every element type is 4- or 8-B, so 4-B granules always tile a segment).
+struct CopyList {
+    const void* src[kMaxSegs];
+    void* dst[kMaxSegs];
+    long long bytes[kMaxSegs];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void multi_copy_kernel(CopyList l) {
+    const int s = blockIdx.y;
+    if (s >= l.n) return;
+    const char* src = (const char*)l.src[s];
+    char* dst = (char*)l.dst[s];
+    const long long nb = l.bytes[s];
+    const long long tid = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+    if ((((uintptr_t)src | (uintptr_t)dst | (uintptr_t)nb) & 15) == 0) {
+        const uint4* s4 = (const uint4*)src;
+        uint4* d4 = (uint4*)dst;
+        for (long long i = tid; i < nb / 16; i += stride) d4[i] = s4[i];
+    } else {
+        const unsigned* s1 = (const unsigned*)src;
+        unsigned* d1 = (unsigned*)dst;
+        for (long long i = tid; i < nb / 4; i += stride) d1[i] = s1[i];
+    }
+}
+
+int launch_copies(const CopyList& l, hipStream_t s) {
+    if (l.n == 0) return 0;
+    long long mx = 0;
+    for (int i = 0; i < l.n; ++i) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+    unsigned gx = cdiv((size_t)(mx / 16 + 1), 256);
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(multi_copy_kernel, dim3(gx, l.n), dim3(256), 0, s, l);
+    CME_TRY(hipGetLastError());
+    return 0;
+}
+
+// ---------------------------------------------------- cross-process epochs
+// Pass e of the IPC transport is ordered across processes by 32-bit epoch
+// words in device memory every peer maps:
+//   flags[0]      = e   : "my blocks of pass e are packed, my rows written"
+//   flags[1 + j]  = e   : "neighbour j has pulled pass e from me"
+// A signal kernel stores them (system-scope atomic stores, written through to
+// memory: a plain store behind a fence is never seen by another XCD -- see
+// cdna_hip_programming.md §6 G16); a one-wave wait kernel polls them with
+// relaxed system-scope loads and s_sleep, bounded: a peer that never signals
+// sets the sticky timeout word instead of hanging the GPU, and every later
+// wait returns at once. Payload visibility needs no in-kernel fences: the
+// producing kernels have ENDED (end-of-kernel release) before the signal
+// kernel runs, and the consuming copy kernel starts (dispatch acquire) after
+// the wait kernel has seen the epoch.
+constexpr int kMaxPeers = 8;
+constexpr unsigned kSpinLimit = 1u << 23;  // x (poll + ~0.2 us sleep): seconds, not forever
+
+struct FlagList {
+    unsigned* f[kMaxPeers + 1];
+    int n;
+};
+
+__global__ __launch_bounds__(64) void ipc_signal_kernel(FlagList l, unsigned value) {
+    const int i = threadIdx.x;
+    if (i < l.n) __hip_atomic_store(l.f[i], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void ipc_wait_kernel(FlagList l, unsigned value, unsigned* timeout) {
+    const int i = threadIdx.x;
+    if (i >= l.n) return;
+    if (__hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // sticky
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned v = __hip_atomic_load(l.f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((int)(v - value) >= 0) break;  // wrap-safe "v >= value"
+        if (spins >= kSpinLimit) {
+            __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+    }
+}
+
+int launch_signal(const FlagList& l, unsigned v, hipStream_t s) {
+    if (l.n == 0) return 0;
+    hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, s, l, v);
+    CME_TRY(hipGetLastError());
+    return 0;
+}
+
+int launch_wait(const FlagList& l, unsigned v, unsigned* timeout, hipStream_t s) {
+    if (l.n == 0) return 0;
+    hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, l, v, timeout);
+    CME_TRY(hipGetLastError());
+    return 0;
 }
 
 // single step: streaming kernel, exact (variant 2) or FMA (variant 6)
@@ -185,9 +375,29 @@ int stepn_regions<double>(const double* p, double* c, int pitch, int gy, const i
 }
 
 // ------------------------------------------------------------- distributed loop
-// One descriptor per subdomain owned by this process (1 with RCCL; any number
-// with the loopback transport, where every neighbour lives in this process).
-// Layout must match SubDesc in models/heat2d_dist.py.
+// IPC view of one neighbouring process (layout mirrored by IpcPeerDesc in
+// models/heat2d_dist.py).
+struct IpcPeerDesc {
+    void* buf[2];     // its grid states, mapped into this process
+    void* stage;      // its staging buffer (the send half is what we pull)
+    unsigned* flags;  // its epoch words
+    int rank;         // its global rank
+    int slot;         // our index among ITS neighbours (its flags[1 + slot])
+};
+
+struct IpcPlan {
+    unsigned* flags;          // ours: [0] ready epoch, [1 + j] consumed by our neighbour j
+    unsigned* timeout;        // ours: sticky give-up word of the wait kernels
+    long long* epoch;         // host: passes exchanged so far (persists across calls)
+    const long long* row_src; // per rows[i]: the peer's send offset (elements of its grid state)
+    const long long* blk_src; // per blks[i]: the peer's staging offset of the block it sends us
+    int npeer;
+    IpcPeerDesc peer[kMaxPeers];
+};
+
+// One descriptor per subdomain owned by this process (1 with RCCL / IPC; any
+// number with the loopback transport, where every neighbour lives in this
+// process). Layout must match SubDesc in models/heat2d_dist.py.
 struct SubDesc {
     void* buf[2];
     int pitch, gy;
@@ -200,12 +410,63 @@ struct SubDesc {
     int n_rows;
     const int* blks;      // n_blks x {peer, send_x, send_y, recv_x, recv_y, rows, width}
     int n_blks;
-    void* stage;          // RCCL transport: 2 * sum(rows*width) elements
+    void* stage;          // 2 * sum(rows*width) elements: send half, then receive half
     int rank;             // global rank of this subdomain
+    const IpcPlan* ipc;   // transport 3 only
 };
 
 constexpr int kBlk = 7;
 constexpr int kMaxSubs = 64;
+
+// staging offsets of the blocks (send half; the receive half adds `total`)
+long long stage_layout(const SubDesc& d, long long* off) {
+    long long t = 0;
+    for (int i = 0; i < d.n_blks; ++i) {
+        off[i] = t;
+        t += (long long)d.blks[i * kBlk + 5] * d.blks[i * kBlk + 6];
+    }
+    return t;
+}
+
+template <typename T>
+int pack_blocks(const SubDesc& d, T* g, hipStream_t s) {
+    if (d.n_blks == 0) return 0;
+    if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+    BlkList l;
+    l.n = d.n_blks;
+    long long off[kMaxPieces];
+    stage_layout(d, off);
+    int mx = 0;
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
+        l.x[i] = c[1], l.y[i] = c[2], l.rows[i] = c[5], l.width[i] = c[6], l.off[i] = off[i];
+        mx = c[5] * c[6] > mx ? c[5] * c[6] : mx;
+    }
+    hipLaunchKernelGGL((blocks_kernel<T, true>), dim3(cdiv(mx, 256) < 32 ? cdiv(mx, 256) : 32, l.n), dim3(256), 0,
+                       s, g, d.pitch, (T*)d.stage, l);
+    CME_TRY(hipGetLastError());
+    return 0;
+}
+
+template <typename T>
+int unpack_blocks(const SubDesc& d, T* g, hipStream_t s) {
+    if (d.n_blks == 0) return 0;
+    if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+    BlkList l;
+    l.n = d.n_blks;
+    long long off[kMaxPieces];
+    const long long total = stage_layout(d, off);
+    int mx = 0;
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
+        l.x[i] = c[3], l.y[i] = c[4], l.rows[i] = c[5], l.width[i] = c[6], l.off[i] = total + off[i];
+        mx = c[5] * c[6] > mx ? c[5] * c[6] : mx;
+    }
+    hipLaunchKernelGGL((blocks_kernel<T, false>), dim3(cdiv(mx, 256) < 32 ? cdiv(mx, 256) : 32, l.n), dim3(256), 0,
+                       s, g, d.pitch, (T*)d.stage, l);
+    CME_TRY(hipGetLastError());
+    return 0;
+}
 
 // Per-subdomain streams and events. Events for border / interior completion
 // are double-buffered by pass parity so that a pass can wait on the PREVIOUS
@@ -213,7 +474,7 @@ constexpr int kMaxSubs = 64;
 struct SubCtx {
     hipStream_t compute = nullptr, border = nullptr, comm = nullptr;
     hipEvent_t ev_border[2] = {nullptr, nullptr}, ev_int[2] = {nullptr, nullptr}, ev_comm = nullptr;
-    hipEvent_t ev_start = nullptr;
+    hipEvent_t ev_start = nullptr, ev_pack = nullptr;
 };
 
 struct DistCtx {
@@ -246,53 +507,36 @@ int get_ctx(int nsub, DistCtx** out) {
         }
         CME_TRY(hipEventCreateWithFlags(&u.ev_comm, hipEventDisableTiming));
         CME_TRY(hipEventCreateWithFlags(&u.ev_start, hipEventDisableTiming));
+        CME_TRY(hipEventCreateWithFlags(&u.ev_pack, hipEventDisableTiming));
     }
     if (nsub > c.nsub) c.nsub = nsub;
     *out = &c;
     return 0;
 }
 
-// RCCL transport: one grouped send/recv batch on the sub's comm stream.
-// Staged blocks are packed into `stage` first and unpacked after the group.
+// RCCL transport: pack -> one grouped send/recv batch -> unpack, all on the
+// sub's comm stream.
 template <typename T>
 int post_exchange_rccl(ncclComm_t comm, const SubDesc& d, T* g, ncclDataType_t dt, hipStream_t cs) {
     T* stage = (T*)d.stage;
-    long long total = 0;
-    for (int i = 0; i < d.n_blks; ++i) total += (long long)d.blks[i * kBlk + 5] * d.blks[i * kBlk + 6];
-    long long off = 0;
-    for (int i = 0; i < d.n_blks; ++i) {
-        const int* c = d.blks + i * kBlk;
-        const int cnt = c[5] * c[6];
-        hipLaunchKernelGGL(pack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, d.pitch, c[1], c[2], c[5],
-                           c[6], stage + off);
-        off += cnt;
-    }
-    CME_TRY(hipGetLastError());
+    long long off[kMaxPieces];
+    if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+    const long long total = stage_layout(d, off);
+    CME_TRY_INT(pack_blocks<T>(d, g, cs));
     NCCL_TRY(ncclGroupStart());
     for (int i = 0; i < d.n_rows; ++i) {
         const long long* r = d.rows + i * 4;
         NCCL_TRY(ncclSend(g + r[1], (size_t)r[3], dt, (int)r[0], comm, cs));
         NCCL_TRY(ncclRecv(g + r[2], (size_t)r[3], dt, (int)r[0], comm, cs));
     }
-    off = 0;
     for (int i = 0; i < d.n_blks; ++i) {
         const int* c = d.blks + i * kBlk;
         const long long cnt = (long long)c[5] * c[6];
-        NCCL_TRY(ncclSend(stage + off, (size_t)cnt, dt, c[0], comm, cs));
-        NCCL_TRY(ncclRecv(stage + total + off, (size_t)cnt, dt, c[0], comm, cs));
-        off += cnt;
+        NCCL_TRY(ncclSend(stage + off[i], (size_t)cnt, dt, c[0], comm, cs));
+        NCCL_TRY(ncclRecv(stage + total + off[i], (size_t)cnt, dt, c[0], comm, cs));
     }
     NCCL_TRY(ncclGroupEnd());
-    off = 0;
-    for (int i = 0; i < d.n_blks; ++i) {
-        const int* c = d.blks + i * kBlk;
-        const int cnt = c[5] * c[6];
-        hipLaunchKernelGGL(unpack_block_kernel<T>, dim3(cdiv(cnt, 256)), dim3(256), 0, cs, g, d.pitch, c[3], c[4], c[5],
-                           c[6], stage + total + off);
-        off += cnt;
-    }
-    CME_TRY(hipGetLastError());
-    return 0;
+    return unpack_blocks<T>(d, g, cs);
 }
 
 int find_sub(const SubDesc* subs, int nsub, int rank) {
@@ -301,39 +545,110 @@ int find_sub(const SubDesc* subs, int nsub, int rank) {
     return -1;
 }
 
-// Loopback transport: PULL every halo of sub `si` (state k) from the owning
-// neighbour's matching send region with device copies on si's comm stream.
+// Loopback "move": pull every row of sub si (state k) straight from the
+// owning neighbour's grid and every block from the neighbour's staging (which
+// that neighbour packed on its own comm stream -- the caller orders this after
+// every peer's ev_pack).
 template <typename T>
-int post_exchange_loopback(const SubDesc* subs, int nsub, int si, int k, hipStream_t cs) {
+int pull_loopback(const SubDesc* subs, int nsub, int si, int k, hipStream_t cs) {
     const SubDesc& d = subs[si];
     T* g = (T*)d.buf[k];
+    CopyList l;
+    l.n = 0;
     for (int i = 0; i < d.n_rows; ++i) {
         const long long* r = d.rows + i * 4;
         const int pj = find_sub(subs, nsub, (int)r[0]);
-        if (pj < 0) return (int)hipErrorInvalidValue;
+        if (pj < 0 || l.n >= kMaxSegs) return (int)hipErrorInvalidValue;
         const SubDesc& pd = subs[pj];
         long long src_off = -1;
         for (int j = 0; j < pd.n_rows; ++j)
             if (pd.rows[j * 4] == d.rank) src_off = pd.rows[j * 4 + 1];
         if (src_off < 0) return (int)hipErrorInvalidValue;
-        CME_TRY(hipMemcpyAsync(g + r[2], (T*)pd.buf[k] + src_off, (size_t)r[3] * sizeof(T), hipMemcpyDeviceToDevice,
-                               cs));
+        l.src[l.n] = (const T*)pd.buf[k] + src_off;
+        l.dst[l.n] = g + r[2];
+        l.bytes[l.n++] = r[3] * (long long)sizeof(T);
     }
+    long long off[kMaxPieces], poff[kMaxPieces];
+    if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+    const long long total = stage_layout(d, off);
     for (int i = 0; i < d.n_blks; ++i) {
         const int* c = d.blks + i * kBlk;
         const int pj = find_sub(subs, nsub, c[0]);
-        if (pj < 0) return (int)hipErrorInvalidValue;
+        if (pj < 0 || l.n >= kMaxSegs) return (int)hipErrorInvalidValue;
         const SubDesc& pd = subs[pj];
-        const int* m = nullptr;
+        if (pd.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+        stage_layout(pd, poff);
+        int m = -1;
         for (int j = 0; j < pd.n_blks; ++j)
-            if (pd.blks[j * kBlk] == d.rank) m = pd.blks + j * kBlk;
-        if (!m || m[5] != c[5] || m[6] != c[6]) return (int)hipErrorInvalidValue;
-        const T* src = (const T*)pd.buf[k] + (size_t)m[2] * pd.pitch + m[1];
-        T* dst = g + (size_t)c[4] * d.pitch + c[3];
-        CME_TRY(hipMemcpy2DAsync(dst, (size_t)d.pitch * sizeof(T), src, (size_t)pd.pitch * sizeof(T),
-                                 (size_t)c[6] * sizeof(T), (size_t)c[5], hipMemcpyDeviceToDevice, cs));
+            if (pd.blks[j * kBlk] == d.rank) m = j;
+        if (m < 0 || pd.blks[m * kBlk + 5] != c[5] || pd.blks[m * kBlk + 6] != c[6]) return (int)hipErrorInvalidValue;
+        l.src[l.n] = (const T*)pd.stage + poff[m];
+        l.dst[l.n] = (T*)d.stage + total + off[i];
+        l.bytes[l.n++] = (long long)c[5] * c[6] * (long long)sizeof(T);
     }
-    return 0;
+    return launch_copies(l, cs);
+}
+
+// IPC transport, pass epoch e, entirely on the sub's comm stream:
+//   wait  our flags[1..] >= e-1  every neighbour has pulled pass e-1 (our
+//                                staging may be rewritten)
+//   pack  our blocks             -> staging send half
+//   signal our flags[0] = e      rows (written by the border sweep the comm
+//                                stream already waited for) + blocks ready
+//   wait  every peer's flags[0] >= e
+//   pull  rows from peers' grids, blocks from peers' staging
+//   signal peer.flags[1 + slot] = e  (we are done reading them)
+//   unpack
+// Rows we send are re-written two passes later by our border sweep, which is
+// ordered after this exchange's first wait of the NEXT pass (e+1 waits
+// consumed >= e) through the border stream's wait on our ev_comm.
+template <typename T>
+int post_exchange_ipc(const SubDesc& d, int k, unsigned e, hipStream_t cs) {
+    const IpcPlan* P = d.ipc;
+    if (!P || P->npeer > kMaxPeers) return (int)hipErrorInvalidValue;
+    T* g = (T*)d.buf[k];
+    FlagList mine, ready, done, own_ready;
+    mine.n = ready.n = done.n = 0;
+    own_ready.n = 1;
+    own_ready.f[0] = P->flags;
+    for (int j = 0; j < P->npeer; ++j) {
+        mine.f[mine.n++] = P->flags + 1 + j;
+        ready.f[ready.n++] = P->peer[j].flags;
+        done.f[done.n++] = P->peer[j].flags + 1 + P->peer[j].slot;
+    }
+    if (e > 1) CME_TRY_INT(launch_wait(mine, e - 1, P->timeout, cs));
+    CME_TRY_INT(pack_blocks<T>(d, g, cs));
+    CME_TRY_INT(launch_signal(own_ready, e, cs));
+    CME_TRY_INT(launch_wait(ready, e, P->timeout, cs));
+    auto peer_of = [&](int rank) -> int {
+        for (int j = 0; j < P->npeer; ++j)
+            if (P->peer[j].rank == rank) return j;
+        return -1;
+    };
+    CopyList l;
+    l.n = 0;
+    for (int i = 0; i < d.n_rows; ++i) {
+        const long long* r = d.rows + i * 4;
+        const int j = peer_of((int)r[0]);
+        if (j < 0 || l.n >= kMaxSegs) return (int)hipErrorInvalidValue;
+        l.src[l.n] = (const T*)P->peer[j].buf[k] + P->row_src[i];
+        l.dst[l.n] = g + r[2];
+        l.bytes[l.n++] = r[3] * (long long)sizeof(T);
+    }
+    long long off[kMaxPieces];
+    if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
+    const long long total = stage_layout(d, off);
+    for (int i = 0; i < d.n_blks; ++i) {
+        const int* c = d.blks + i * kBlk;
+        const int j = peer_of(c[0]);
+        if (j < 0 || l.n >= kMaxSegs) return (int)hipErrorInvalidValue;
+        l.src[l.n] = (const T*)P->peer[j].stage + P->blk_src[i];
+        l.dst[l.n] = (T*)d.stage + total + off[i];
+        l.bytes[l.n++] = (long long)c[5] * c[6] * (long long)sizeof(T);
+    }
+    CME_TRY_INT(launch_copies(l, cs));
+    CME_TRY_INT(launch_signal(done, e, cs));
+    return unpack_blocks<T>(d, g, cs);
 }
 
 // peers of sub si that live in this process (loopback dependencies)
@@ -365,7 +680,9 @@ template <typename T>
 int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int order, T xcfl, T ycfl, int iters,
              int cur, int sync, int exchange_first, int tblock, int fma, int* cur_out, hipStream_t s) {
     if (nsub < 1 || nsub > kMaxSubs) return (int)hipErrorInvalidValue;
-    if (transport == 0 && nsub != 1) return (int)hipErrorInvalidValue;
+    if ((transport == 0 || transport == 3) && nsub != 1) return (int)hipErrorInvalidValue;
+    if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
+    if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
     if (tblock < 1 || tblock > 4 || (tblock > 2 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
     // 0 (default): border stream || interior stream; 1: border then interior
     // on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
@@ -381,13 +698,30 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     int peers[kMaxSubs][16];
     int npeer[kMaxSubs];
     for (int si = 0; si < nsub; ++si) {
+        if (subs[si].n_rows + subs[si].n_blks > 16) return (int)hipErrorInvalidValue;
         npeer[si] = local_peers(subs, nsub, si, peers[si]);
         if (transport == 1 && npeer[si] != subs[si].n_rows + subs[si].n_blks) return (int)hipErrorInvalidValue;
     }
-    auto exchange = [&](int si, int k) -> int {
-        if (transport == 0) return post_exchange_rccl<T>(comm, subs[si], (T*)subs[si].buf[k], dt, ctx->sub[si].comm);
-        if (transport == 1) return post_exchange_loopback<T>(subs, nsub, si, k, ctx->sub[si].comm);
-        return 0;  // transport 2: no exchange (benchmarking the compute schedule)
+    long long epoch = (transport == 3) ? *subs[0].ipc->epoch : 0;
+    // Exchange the halos of state k for every sub. The caller has made each
+    // comm stream wait for what the exchange reads; ev_comm is recorded after.
+    auto exchange_all = [&](int k) -> int {
+        if (transport == 0)
+            return post_exchange_rccl<T>(comm, subs[0], (T*)subs[0].buf[k], dt, ctx->sub[0].comm);
+        if (transport == 3) return post_exchange_ipc<T>(subs[0], k, (unsigned)(++epoch), ctx->sub[0].comm);
+        if (transport == 2) return 0;
+        for (int si = 0; si < nsub; ++si) {  // loopback: pack everything, then pull
+            CME_TRY_INT(pack_blocks<T>(subs[si], (T*)subs[si].buf[k], ctx->sub[si].comm));
+            CME_TRY(hipEventRecord(ctx->sub[si].ev_pack, ctx->sub[si].comm));
+        }
+        for (int si = 0; si < nsub; ++si) {
+            SubCtx& u = ctx->sub[si];
+            for (int j = 0; j < npeer[si]; ++j)
+                CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_pack, 0));
+            CME_TRY_INT(pull_loopback<T>(subs, nsub, si, k, u.comm));
+            CME_TRY_INT(unpack_blocks<T>(subs[si], (T*)subs[si].buf[k], u.comm));
+        }
+        return 0;
     };
     auto sweep = [&](int si, const int* regs, int n, int k, int ns, hipStream_t st) -> int {
         const SubDesc& d = subs[si];
@@ -411,11 +745,24 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         CME_TRY(hipStreamWaitEvent(u.comm, u.ev_start, 0));
     }
     if (exchange_first) {  // make the halos of the current state valid
-        for (int si = 0; si < nsub; ++si) CME_TRY_INT(exchange(si, cur));
+        CME_TRY_INT(exchange_all(cur));
         for (int si = 0; si < nsub; ++si) CME_TRY(hipEventRecord(ctx->sub[si].ev_comm, ctx->sub[si].comm));
         for (int si = 0; si < nsub; ++si)
             for (int j = 0; j < nsub; ++j) CME_TRY(hipStreamWaitEvent(ctx->sub[si].compute, ctx->sub[j].ev_comm, 0));
     }
+    // comm streams wait this pass's border strips (own + local neighbours'),
+    // then the exchange of the state those strips completed
+    auto post_comm = [&](int par, int k) -> int {
+        for (int si = 0; si < nsub; ++si) {
+            SubCtx& u = ctx->sub[si];
+            CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
+            for (int j = 0; j < npeer[si]; ++j)
+                CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
+        }
+        CME_TRY_INT(exchange_all(k));
+        for (int si = 0; si < nsub; ++si) CME_TRY(hipEventRecord(ctx->sub[si].ev_comm, ctx->sub[si].comm));
+        return 0;
+    };
     int pass = 0;
     for (int it = 0; it < iters; ++pass) {
         // timesteps in this pass: tblock, or what is left (a tail pass of
@@ -429,14 +776,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
-            for (int si = 0; si < nsub; ++si) {
-                SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
-                for (int j = 0; j < npeer[si]; ++j)
-                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
-                CME_TRY_INT(exchange(si, cur ^ 1));
-                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
-            }
+            CME_TRY_INT(post_comm(par, cur ^ 1));
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
                 CME_TRY(hipStreamWaitEvent(u.compute, u.ev_comm, 0));
@@ -454,14 +794,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
-            for (int si = 0; si < nsub; ++si) {
-                SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
-                for (int j = 0; j < npeer[si]; ++j)
-                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
-                CME_TRY_INT(exchange(si, cur ^ 1));
-                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
-            }
+            CME_TRY_INT(post_comm(par, cur ^ 1));
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
                 CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
@@ -477,14 +810,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.border));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.border));
             }
-            for (int si = 0; si < nsub; ++si) {  // halo exchange of the new state
-                SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.comm, u.ev_border[par], 0));
-                for (int j = 0; j < npeer[si]; ++j)
-                    CME_TRY(hipStreamWaitEvent(u.comm, ctx->sub[peers[si][j]].ev_border[par], 0));
-                CME_TRY_INT(exchange(si, cur ^ 1));
-                CME_TRY(hipEventRecord(u.ev_comm, u.comm));
-            }
+            CME_TRY_INT(post_comm(par, cur ^ 1));  // halo exchange of the new state
             for (int si = 0; si < nsub; ++si) {  // deep interior, overlapping both
                 SubCtx& u = ctx->sub[si];
                 CME_TRY(hipStreamWaitEvent(u.compute, u.ev_border[par ^ 1], 0));
@@ -504,6 +830,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         CME_TRY(hipStreamWaitEvent(s, u.ev_border[0], 0));
         CME_TRY(hipStreamWaitEvent(s, u.ev_comm, 0));
     }
+    if (transport == 3) *subs[0].ipc->epoch = epoch;
     *cur_out = cur;
     return 0;
 }
@@ -512,7 +839,8 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
 
 // The distributed heat loop (see dist_run). transport 0 = RCCL (`comm`, one
 // sub), 1 = loopback (every neighbour is one of `subs`), 2 = none (halos are
-// not exchanged; benchmarks/bench_dist_rank.py). dtype 0 f32, 1 f64.
+// not exchanged; benchmarks/bench_dist_rank.py), 3 = IPC (one sub per
+// process, neighbours' memory mapped through SubDesc.ipc). dtype 0 f32, 1 f64.
 // tblock n (1-4): n steps per exchange (nB-deep halos, `interior` shrunk by
 // nB on neighbour sides, `ext` = owned region grown by (n-1)B on neighbour
 // sides; 3 and 4 fp32 only). fma: FMA-contracted stencil.
@@ -528,4 +856,17 @@ CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, in
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(halo_pack_f32, 256, pack_block_kernel<float>);
+CME_REGISTER_KERNEL(halo_pack_f32, 256, blocks_kernel<float, true>);
+CME_REGISTER_KERNEL(halo_copy, 256, multi_copy_kernel);
+CME_REGISTER_KERNEL(ipc_wait, 64, ipc_wait_kernel);
+
+// ABI check for the ctypes mirrors in models/heat2d_dist.py (tests/test_protos.py):
+// {sizeof SubDesc, offsetof SubDesc.ipc, sizeof IpcPeerDesc, sizeof IpcPlan, offsetof IpcPlan.peer}
+CME_EXPORT int cme_dist_abi(long long* out) {
+    out[0] = (long long)sizeof(SubDesc);
+    out[1] = (long long)offsetof(SubDesc, ipc);
+    out[2] = (long long)sizeof(IpcPeerDesc);
+    out[3] = (long long)sizeof(IpcPlan);
+    out[4] = (long long)offsetof(IpcPlan, peer);
+    return 0;
+}

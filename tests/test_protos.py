@@ -44,3 +44,17 @@ def test_prototypes_match_native_signatures():
             assert sig.replace(" ", "") == sigs[name], f"{name}: proto {sig} != native {sigs[name]}"
             checked += 1
     assert checked > 20
+
+
+def test_dist_abi_matches_ctypes_mirrors():
+    """The ctypes mirrors of SubDesc / IpcPlan / IpcPeerDesc must have the
+    native layout: the native loop reads them field by field."""
+    import ctypes
+
+    from cme213x.models.heat2d_dist import IpcPeerDesc, IpcPlan, SubDesc
+
+    _ext.proto(_ext.HIP_PROTOS, "cme_dist_abi", "p")
+    out = (ctypes.c_longlong * 5)()
+    _ext.call_hip("cme_dist_abi", ctypes.addressof(out))
+    assert list(out) == [ctypes.sizeof(SubDesc), SubDesc.ipc.offset, ctypes.sizeof(IpcPeerDesc),
+                         ctypes.sizeof(IpcPlan), IpcPlan.peer.offset]
