@@ -230,18 +230,20 @@ class LoopbackComm(Comm):
         pass
 
 
-def init_from_env(device_type: str | None = None) -> Comm:
+def init_from_env(device_type: str | None = None, backend: str | None = None, share_gpu: bool = False) -> Comm:
     """torchrun-style bootstrap (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT).
-    Returns :class:`LoopbackComm` when WORLD_SIZE is unset or 1."""
+    Returns :class:`LoopbackComm` when WORLD_SIZE is unset or 1.
+    ``share_gpu``: every rank on device 0 (rehearsing a multi-rank run on one
+    GPU; RCCL refuses that, so pair it with ``backend="gloo"``)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1:
         return LoopbackComm()
     if not dist.is_initialized():
         if device_type is None:
             device_type = "cuda" if torch.cuda.is_available() else "cpu"
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        backend = backend or ("nccl" if device_type == "cuda" else "gloo")
         if device_type == "cuda":
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            torch.cuda.set_device(0 if share_gpu else int(os.environ.get("LOCAL_RANK", "0")))
         kw = {}
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())

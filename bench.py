@@ -10,10 +10,10 @@ EXACTLY K timed steps bracketed by barrier + synchronize, max over ranks; rank
 A "step" is one full timestep of the global grid: the FTCS sweep of every
 point plus the halo exchange between neighbouring ranks (1-D stripes, async
 mode: deep interior overlapped with the exchange, borders after it). With
-``--tblock 3`` (default) three timesteps are fused into one HBM pass
-(temporal blocking) and each exchange moves 3B-deep halos; K timed steps are
-still exactly K timesteps (a K that is not a multiple of 3 ends with a shorter
-pass).
+``--tblock n`` (default: 3, or 4 when a rank holds <= 1/8 of 16384^2 --
+``auto_tblock``) n timesteps are fused into one HBM pass (temporal blocking)
+and each exchange moves nB-deep halos; K timed steps are still exactly K
+timesteps (a K that is not a multiple of n ends with a shorter pass).
 
 Metric convention: effective GB/s = points x 72 B (17 taps + 1
 store, fp32) per iteration / time -- the convention the reference's 240 GB/s
@@ -93,6 +93,17 @@ def native_selftest(comm, native, dev, args) -> bool:
     return bool(bad.item() == 0)
 
 
+def auto_tblock(points_per_rank: int) -> int:
+    """Timesteps per pass for a subdomain size. Every wave of the fused pass
+    re-computes 2(NS-1)B warm-up rows, a per-pass cost fixed by the resident
+    wave count, not by the subdomain; a small subdomain amortises it over
+    more steps. Measured one-rank schedules (benchmarks/bench_dist_rank.py,
+    profiles/dist_rank_r2.md): 3 steps win at 16384^2 / 1, 2, 4 ranks
+    (0.181 / 0.0996 / 0.0584 ms/step vs 0.193 / 0.104 / 0.0596), 4 steps at
+    8 ranks (0.0307 vs 0.0321-0.0336)."""
+    return 4 if points_per_rank <= 16384 * 16384 // 8 else 3
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,8 +120,9 @@ def main() -> int:
     ap.add_argument("--fma", type=int, choices=[0, 1], default=1,
                     help="FMA-contracted stencil (what nvcc emits for the reference's GPU kernels); 0 = exact "
                          "contraction-off arithmetic, bitwise equal to the non-FMA CPU oracle")
-    ap.add_argument("--tblock", type=int, choices=[1, 2, 3, 4], default=3,
-                    help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos)")
+    ap.add_argument("--tblock", type=int, choices=[0, 1, 2, 3, 4], default=0,
+                    help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos); "
+                         "0 = by subdomain size (auto_tblock)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: run the K-step loop in C++ over a native communicator (auto: after a "
                          "bitwise self-test against the torch.distributed loop)")
@@ -120,7 +132,12 @@ def main() -> int:
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
                          "(tests; never the reported number)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0 with a gloo control plane and the IPC transport "
+                         "(exercises the multi-rank flow on a 1-GPU box; the number is not a scaling result)")
     args = ap.parse_args()
+    if args.share_gpu:
+        args.transport = "ipc"
 
     import torch
     import torch.distributed as dist
@@ -137,7 +154,7 @@ def main() -> int:
               "torch.distributed.run with --nproc-per-node equal to --gpus", file=sys.stderr)
         return 2
     on_gpu = args.device == "cuda"
-    comm = init_from_env(args.device)
+    comm = init_from_env(args.device, backend="gloo" if args.share_gpu else None, share_gpu=args.share_gpu)
     rank = comm.rank
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
 
@@ -145,6 +162,8 @@ def main() -> int:
         if on_gpu:
             torch.cuda.synchronize(dev)
 
+    if args.tblock == 0:
+        args.tblock = auto_tblock(args.n * args.n // max(1, comm.size))
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
@@ -185,7 +204,7 @@ def main() -> int:
                 if native is not None and args.transport == "rccl":
                     native.abort()  # pending native sends/recvs fail on the peers instead of hanging
             native_ok = agree(native_ok)
-        if not native_ok and args.native == "on":
+        if not native_ok and (args.native == "on" or args.share_gpu):
             print("bench.py: --native on but the native loop failed", file=sys.stderr)
             return 3
     use_native = native is not None and native_ok
@@ -276,6 +295,7 @@ def main() -> int:
                 "fma": bool(args.fma),
                 "tblock": args.tblock,
                 "device": args.device,
+                "rehearsal_shared_gpu": bool(args.share_gpu),
                 "loop": f"native-{args.transport}" if use_native else ("torch.distributed" if comm.size > 1
                                                                          else "single"),
             },

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--fma", type=int, default=1)
     ap.add_argument("--tblock", type=int, default=3, help="timesteps per exchange / HBM pass (1-4)")
     ap.add_argument("--native", type=int, default=1, help="1: native loop (null transport); 0: Python loop")
+    ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     import torch
 
@@ -60,16 +61,20 @@ def main():
             else:
                 sim.run(k)
 
-        run(10)
+        run(30)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        run(args.steps)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / args.steps
+        times = []
+        for _ in range(args.reps):  # median of reps (clock / thermal noise is +-5 % per rep)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run(args.steps)
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) / args.steps)
+        ms = sorted(times)[len(times) // 2]
         base = base or ms * w
         print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
+                          "reps": args.reps,
                           "ms_per_step": round(ms, 4),
                           "compute_scaling_eff": round(base / (ms * w), 3)}), flush=True)
         del sim

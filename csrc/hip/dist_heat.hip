@@ -257,9 +257,20 @@ struct CopyList {
     int n;
 };
 
+template <bool kSysAcquire>
 __global__ __launch_bounds__(256) void multi_copy_kernel(CopyList l) {
     const int s = blockIdx.y;
     if (s >= l.n) return;
+    if constexpr (kSysAcquire) {
+        // IPC pull: peer memory (over xGMI) may sit in this XCD's L2 from an
+        // earlier pass; a system-scope acquire drops those lines before the
+        // loads (one lane fences, the barrier holds the block behind it).
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
     const char* src = (const char*)l.src[s];
     char* dst = (char*)l.dst[s];
     const long long nb = l.bytes[s];
@@ -275,13 +286,16 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(CopyList l) {
     }
 }
 
-int launch_copies(const CopyList& l, hipStream_t s) {
+int launch_copies(const CopyList& l, hipStream_t s, bool sys_acquire = false) {
     if (l.n == 0) return 0;
     long long mx = 0;
     for (int i = 0; i < l.n; ++i) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
     unsigned gx = cdiv((size_t)(mx / 16 + 1), 256);
     if (gx > 64) gx = 64;
-    hipLaunchKernelGGL(multi_copy_kernel, dim3(gx, l.n), dim3(256), 0, s, l);
+    if (sys_acquire)
+        hipLaunchKernelGGL(multi_copy_kernel<true>, dim3(gx, l.n), dim3(256), 0, s, l);
+    else
+        hipLaunchKernelGGL(multi_copy_kernel<false>, dim3(gx, l.n), dim3(256), 0, s, l);
     CME_TRY(hipGetLastError());
     return 0;
 }
@@ -501,13 +515,23 @@ int get_ctx(int nsub, DistCtx** out) {
         CME_TRY(hipStreamCreateWithFlags(&u.compute, hipStreamNonBlocking));
         CME_TRY(hipStreamCreateWithPriority(&u.border, hipStreamNonBlocking, greatest));
         CME_TRY(hipStreamCreateWithPriority(&u.comm, hipStreamNonBlocking, greatest));
+        // The events only order streams of THIS device, so a device-scope
+        // release would do; measured on one N=8 subdomain (profiles/
+        // dist_rank_r2.md) the default system-scope record is no slower
+        // (0.0321-0.0322 vs 0.0334-0.0338 ms/step), so it stays the default.
+        // CME_DIST_EVENT_SCOPE=device selects hipEventReleaseToDevice.
+        static const unsigned evf = [] {
+            const char* e = getenv("CME_DIST_EVENT_SCOPE");
+            return (e && strcmp(e, "device") == 0) ? (unsigned)(hipEventDisableTiming | hipEventReleaseToDevice)
+                                                   : (unsigned)hipEventDisableTiming;
+        }();
         for (int k = 0; k < 2; ++k) {
-            CME_TRY(hipEventCreateWithFlags(&u.ev_border[k], hipEventDisableTiming));
-            CME_TRY(hipEventCreateWithFlags(&u.ev_int[k], hipEventDisableTiming));
+            CME_TRY(hipEventCreateWithFlags(&u.ev_border[k], evf));
+            CME_TRY(hipEventCreateWithFlags(&u.ev_int[k], evf));
         }
-        CME_TRY(hipEventCreateWithFlags(&u.ev_comm, hipEventDisableTiming));
-        CME_TRY(hipEventCreateWithFlags(&u.ev_start, hipEventDisableTiming));
-        CME_TRY(hipEventCreateWithFlags(&u.ev_pack, hipEventDisableTiming));
+        CME_TRY(hipEventCreateWithFlags(&u.ev_comm, evf));
+        CME_TRY(hipEventCreateWithFlags(&u.ev_start, evf));
+        CME_TRY(hipEventCreateWithFlags(&u.ev_pack, evf));
     }
     if (nsub > c.nsub) c.nsub = nsub;
     *out = &c;
@@ -646,7 +670,7 @@ int post_exchange_ipc(const SubDesc& d, int k, unsigned e, hipStream_t cs) {
         l.dst[l.n] = (T*)d.stage + total + off[i];
         l.bytes[l.n++] = (long long)c[5] * c[6] * (long long)sizeof(T);
     }
-    CME_TRY_INT(launch_copies(l, cs));
+    CME_TRY_INT(launch_copies(l, cs, true));
     CME_TRY_INT(launch_signal(done, e, cs));
     return unpack_blocks<T>(d, g, cs);
 }
@@ -857,7 +881,7 @@ CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, in
 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(halo_pack_f32, 256, blocks_kernel<float, true>);
-CME_REGISTER_KERNEL(halo_copy, 256, multi_copy_kernel);
+CME_REGISTER_KERNEL(halo_copy, 256, multi_copy_kernel<false>);
 CME_REGISTER_KERNEL(ipc_wait, 64, ipc_wait_kernel);
 
 // ABI check for the ctypes mirrors in models/heat2d_dist.py (tests/test_protos.py):

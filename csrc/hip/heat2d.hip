@@ -658,23 +658,52 @@ int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region
 // NS-step pass (NS = 3, 4; fp32): rows per block and chunk heights from
 // benchmarks/tune_heatn.py (profiles/heat_streamn_tune.md: at 16384^2 NS=3
 // RB=4 ~190-row chunks 0.178 ms/step, NS=4 RB=2 0.195, stream2 0.237).
-// CME_STREAMN_CHUNK overrides for experiments. Thin regions use the stream2
-// rule (about 1024 waves, latency-bound border strips).
+//
+// Chunk rule, in units of the device's RESIDENT wave capacity `cap` (2 waves
+// per SIMD for NS=3 RB=4): aim for 3 full rounds of waves (16384^2: 71 strips
+// x 86 chunks of ~190 rows); when that makes chunks shorter than `min_chunk`
+// rows -- a strong-scaled subdomain, where every chunk re-computes 2(NS-1)B
+// warm-up rows and re-reads 2NS*B input rows -- use fewer whole rounds (2,
+// then 1) with longer chunks instead of more, shorter ones. A whole number of
+// rounds keeps the tail short. CME_STREAMN_CHUNK / _ROUNDS / _MINCHUNK
+// override for experiments (benchmarks/tune_dist_rank.py). Thin regions
+// (border strips: latency-bound, on the critical path after an exchange) use
+// about 1024 waves.
 template <int NS, int RB>
-int streamn_chunk(int strips, int H, int chunk_hint) {
+int streamn_chunk(int strips, int H, int chunk_hint, long cap) {
     static const int env_chunk = [] {
         const char* e = getenv("CME_STREAMN_CHUNK");
         return e ? atoi(e) : 0;
     }();
+    static const int env_rounds = [] {
+        const char* e = getenv("CME_STREAMN_ROUNDS");
+        return e ? atoi(e) : 0;
+    }();
+    static const int env_min = [] {
+        const char* e = getenv("CME_STREAMN_MINCHUNK");
+        return e ? atoi(e) : 0;
+    }();
+    static const long thin_waves = [] {
+        const char* e = getenv("CME_STREAMN_THIN_WAVES");
+        return e && atoi(e) > 0 ? (long)atoi(e) : 1024L;
+    }();
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
-        const long target_waves = 256L * 24;
-        long rows = ((long)strips * H + target_waves - 1) / target_waves;
         const long lo = 8 * RB > 32 ? 8 * RB : 32;
+        long rows;
         if ((long)strips * cdiv(H, lo) < 1024) {
-            rows = ((long)strips * H + 1023) / 1024;
+            rows = ((long)strips * H + thin_waves - 1) / thin_waves;
             rows = rows < RB ? RB : rows;
         } else {
+            const int max_rounds = env_rounds > 0 ? env_rounds : 3;
+            const long min_chunk = env_min > 0 ? env_min : 64;
+            rows = 0;
+            for (int r = max_rounds; r >= 1; --r) {
+                long per_strip = r * cap / strips;
+                per_strip = per_strip < 1 ? 1 : per_strip;
+                rows = (H + per_strip - 1) / per_strip;
+                if (rows >= min_chunk) break;
+            }
             rows = rows < lo ? lo : rows;
         }
         rows = rows > 1024 ? 1024 : rows;
@@ -689,6 +718,7 @@ int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region
     static_assert(NS >= 3 && NS <= 4, "streamN: 3 or 4 steps per pass");
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
+    static const long cap = resident_waves(heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD>, 256);
     S2Regions R{};
     int waves = 0;
     for (int i = 0; i < n; ++i) {
@@ -696,7 +726,7 @@ int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region
         const int H = g.ye - g.yb;
         if (H <= 0 || g.xe <= g.xb) continue;
         const int strips = (int)cdiv(g.xe - (g.xb & ~3), StripN<NS>::kOut);
-        const int chunk = streamn_chunk<NS, RB>(strips, H, chunk_hint);
+        const int chunk = streamn_chunk<NS, RB>(strips, H, chunk_hint, cap);
         const int k = R.n++;
         R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
         R.strips[k] = strips;

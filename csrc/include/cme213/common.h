@@ -61,6 +61,31 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned bid, unsigned nwg) {
     return base + bid / kNumXCD;
 }
 
+// CUs of the CURRENT device, cached per device: a partitioned MI355X
+// (CPX/DPX modes) or another gfx950 part exposes fewer than 256, so grids
+// that must be co-resident are sized from this, never from kNumCU.
+static inline int device_cu_count() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return kNumCU;
+    int& c = cached[dev & 63];
+    if (c == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = kNumCU;
+        c = v;
+    }
+    return c;
+}
+
+// Waves of `kernel` (launched with `threads` per block) the device holds at
+// once: occupancy-API blocks per CU x CUs x waves per block.
+template <typename K>
+static inline long resident_waves(K kernel, int threads) {
+    int api = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kernel, threads, 0) != hipSuccess || api < 1) api = 1;
+    return (long)api * device_cu_count() * ((threads + kWave - 1) / kWave);
+}
+
 // Co-resident grid for a persistent kernel: min(occupancy API - 1, cap)
 // blocks per CU (the API can over-report by one block per CU on gfx950 for
 // SGPR-heavy kernels -- MI355X_MICROARCH.md "Residency"), at least 1.

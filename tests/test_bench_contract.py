@@ -46,3 +46,28 @@ def test_dist_spmv_bench_cpu(mode):
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
     assert rec["n_gpus"] == 3 and rec["max_abs_err"] < 1e-4
+
+
+def _launch_gpu(nproc, extra):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", str(nproc), "--steps", "20", "--warmup", "3", "--spinup", "0", "--grid", "2048", *extra]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("nproc,extra", [(2, []), (4, ["--method", "2", "--tblock", "4"])])
+def test_bench_multirank_shared_gpu_ipc(gpu, nproc, extra):
+    """The driver's N>1 bench flow (torch.distributed.run, one process per
+    rank, native loop after its bitwise self-test) rehearsed on ONE GPU: every
+    rank on cuda:0, gloo control plane, IPC halo transport."""
+    rec = _launch_gpu(nproc, ["--share-gpu", *extra])
+    assert rec["n_gpus"] == nproc and rec["sanity_ok"] is True
+    assert rec["native_selftest"] is True
+    assert rec["config"]["loop"] == "native-ipc" and rec["config"]["rehearsal_shared_gpu"] is True
