@@ -44,8 +44,10 @@ def monte_carlo_pi(samples: int, seed: int = 1, device="cuda") -> tuple[float, i
 
 
 def global_max(x: torch.Tensor) -> float:
-    if not x.is_cuda:
-        return float(x.max())
+    if not x.is_cuda:  # OpenMP reduction (csrc/cpu/scan_cpu.cpp)
+        from .scan import reduce as _reduce
+
+        return float(_reduce(x.reshape(-1).contiguous(), "max"))
     out = torch.empty(1, dtype=torch.int32, device=x.device)
     _ext.call_hip("cme_global_max", x.data_ptr(), x.numel(), out.data_ptr(), _ext.stream_ptr(x.device))
     i = int(out.item())
@@ -58,9 +60,10 @@ def segment_sums_workqueue(offsets: torch.Tensor, v: torch.Tensor) -> torch.Tens
     """out[s] = sum(v[offsets[s]:offsets[s+1]]), segments dequeued atomically."""
     nseg = offsets.numel() - 1
     out = torch.empty(nseg, dtype=torch.float32, device=v.device)
-    if not v.is_cuda:
-        c = torch.cat([torch.zeros(1, dtype=torch.float64), torch.cumsum(v.double(), 0)])
-        return (c[offsets[1:].long()] - c[offsets[:-1].long()]).float()
+    if not v.is_cuda:  # OpenMP segmented reduction (csrc/cpu/algorithms_cpu.cpp)
+        from .algorithms import segment_reduce
+
+        return segment_reduce(v.contiguous(), offsets.to(torch.int64), "sum")
     head = torch.empty(1, dtype=torch.int32, device=v.device)
     _ext.call_hip("cme_workqueue_segment_sums", offsets.data_ptr(), nseg, v.data_ptr(), out.data_ptr(),
                   head.data_ptr(), _ext.stream_ptr(v.device))

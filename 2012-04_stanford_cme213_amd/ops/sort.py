@@ -15,6 +15,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_u32", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_serial_u32", "ppqi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_merge_sort_i32", "ppqqqp")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_kv_u32", "ppppqii")
 
 
 def _to_u32(k: torch.Tensor) -> torch.Tensor:
@@ -95,7 +96,19 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
             return out, v.view(values.dtype)
         return out
     if values is not None:
-        raise NotImplementedError("CPU key-value sort: use the GPU path")
+        if algo != "radix":
+            raise NotImplementedError("CPU key-value sort: algo='radix'")
+        if values.element_size() != 4 or values.numel() != n:
+            raise TypeError("values: one 32-bit value per key")
+        if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
+            raise TypeError("key_bits < 32 needs non-negative integer keys")
+        k = keys.contiguous().clone().view(torch.uint32) if key_bits < 32 else _to_u32(keys.contiguous())
+        v = values.contiguous().clone().view(torch.uint32)
+        kt, vt = torch.empty_like(k), torch.empty_like(v)
+        _ext.call_cpu("cme_cpu_radix_sort_kv_u32", k.data_ptr(), kt.data_ptr(), v.data_ptr(), vt.data_ptr(), n,
+                      num_bits, min(32, max(1, int(key_bits))))
+        out = k.view(dtype) if key_bits < 32 else _from_u32(k, dtype)
+        return out, v.view(values.dtype)
     if algo == "merge":
         if dtype != torch.int32:
             raise TypeError("CPU merge sort takes int32 keys (the hw4 driver's type)")

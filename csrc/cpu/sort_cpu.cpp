@@ -18,7 +18,9 @@
 
 namespace {
 
-void radix_pass(const uint32_t* in, uint32_t* out, long long n, int shift, int bits, int nblocks) {
+// vin / vout: optional 32-bit values carried with the keys (stable)
+void radix_pass(const uint32_t* in, uint32_t* out, long long n, int shift, int bits, int nblocks,
+                const uint32_t* vin = nullptr, uint32_t* vout = nullptr) {
     const uint32_t nb = 1u << bits, mask = nb - 1;
     std::vector<uint32_t> hist((size_t)nblocks * nb, 0);
     const long long bs = (n + nblocks - 1) / nblocks;
@@ -47,7 +49,15 @@ void radix_pass(const uint32_t* in, uint32_t* out, long long n, int shift, int b
     for (int b = 0; b < nblocks; ++b) {
         uint64_t* o = &off[(size_t)b * nb];
         const long long e = std::min(n, (b + 1) * bs);
-        for (long long i = b * bs; i < e; ++i) out[o[(in[i] >> shift) & mask]++] = in[i];
+        if (vin) {
+            for (long long i = b * bs; i < e; ++i) {
+                const uint64_t d = o[(in[i] >> shift) & mask]++;
+                out[d] = in[i];
+                vout[d] = vin[i];
+            }
+        } else {
+            for (long long i = b * bs; i < e; ++i) out[o[(in[i] >> shift) & mask]++] = in[i];
+        }
     }
 }
 
@@ -110,6 +120,25 @@ CME_CPU_EXPORT int cme_cpu_radix_sort_u32(uint32_t* keys, uint32_t* tmp, long lo
         std::swap(in, out);
     }
     if (in != keys) std::memcpy(keys, in, n * sizeof(uint32_t));
+    return 0;
+}
+
+// Key-value LSD radix sort over the low `key_bits` bits (32 = full keys;
+// fewer = a counting sort for small key ranges, Lecture16). Stable.
+CME_CPU_EXPORT int cme_cpu_radix_sort_kv_u32(uint32_t* keys, uint32_t* ktmp, uint32_t* vals, uint32_t* vtmp,
+                                             long long n, int num_bits, int key_bits) {
+    if (num_bits < 1 || num_bits > 16 || key_bits < 1 || key_bits > 32) return 1;
+    const int nblocks = std::max(1, omp_get_max_threads() * 4);
+    uint32_t *in = keys, *out = ktmp, *vi = vals, *vo = vtmp;
+    for (int shift = 0; shift < key_bits; shift += num_bits) {
+        radix_pass(in, out, n, shift, std::min(num_bits, key_bits - shift), nblocks, vi, vo);
+        std::swap(in, out);
+        std::swap(vi, vo);
+    }
+    if (in != keys) {
+        std::memcpy(keys, in, n * sizeof(uint32_t));
+        std::memcpy(vals, vi, n * sizeof(uint32_t));
+    }
     return 0;
 }
 
