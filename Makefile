@@ -8,7 +8,7 @@ ifeq ($(DEBUG),1)
 export CME_DEBUG = 1
 endif
 
-.PHONY: all build test test-gpu bench smoke occupancy clean
+.PHONY: all build test test-asan test-gpu bench smoke occupancy clean
 
 all: build
 
@@ -17,6 +17,11 @@ build:
 
 test: build
 	$(PY) -m pytest tests -x -q -m "not gpu"
+
+# CPU backend under AddressSanitizer + UBSan (host code only; the course's
+# cuda-memcheck, slides/Lecture06.pdf 2-3): instrumented build in build/asan
+test-asan:
+	$(PY) scripts/asan_cpu.py
 
 # on a machine with an MI355X
 test-gpu: build

@@ -12,7 +12,7 @@ from cme213x.ops.stencil import heat_step_torch
 from cme213x.utils.params import SimParams
 from cme213x.utils.ulp import ulp_distance
 
-REF_PARAMS = "/root/reference/hw/hw2/programming/params_test.in"
+REF_PARAMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "hw2_params_test.in")
 
 
 def _rand_grid(p, dtype, device="cpu", seed=0):

@@ -11,7 +11,7 @@ from cme213x.models.spmv_scan import (SpmvScanSolver, errors, generate, load,
                                       reference_solution, reference_solution_quadratic, run_fp, save)
 from cme213x.ops.scan import head_flags_from_offsets, lookback_timed_out, reduce, scan, segmented_scan
 
-SMALL = "/root/reference/hw/hw_final/programming/aux/CheckOutput"
+SMALL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
 
 def _np_segscan(v, heads):

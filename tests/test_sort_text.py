@@ -10,7 +10,7 @@ from cme213x.ops.sort import merge_sort_cpu, sort
 from cme213x.ops.text import (digraph_histogram, histogram_u8, letter_histogram, match_counts,
                               residue_histograms, sanitize, vigenere)
 
-BOOK = "/root/reference/hw/hw3/programming/mobydick.txt"
+BOOK = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "mobydick_hw3.txt.gz")
 
 
 # English letter frequencies (%), a..z: a synthetic corpus with the same
@@ -21,7 +21,9 @@ _EN = [8.17, 1.49, 2.78, 4.25, 12.70, 2.23, 2.02, 6.09, 6.97, 0.15, 0.77, 4.03, 
 
 def _book():
     if os.path.exists(BOOK):
-        return open(BOOK, "rb").read()
+        import gzip
+
+        return gzip.open(BOOK, "rb").read()
     rng = np.random.default_rng(0)
     p = np.asarray(_EN) / sum(_EN)
     letters = rng.choice(np.arange(97, 123, dtype=np.uint8), size=1_200_000, p=p)
