@@ -48,23 +48,55 @@ def workspace(device: torch.device, nbytes: int, key: str = "lookback") -> torch
 
 
 def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
+    """Descriptor array of a look-back launch. Keyed by (device, STREAM): two
+    scans enqueued on different streams must not zero / overwrite each
+    other's descriptors."""
     tiles = (x.numel() + TILE - 1) // TILE
-    return workspace(x.device, tiles * 8 + 16)
+    return workspace(x.device, tiles * 8 + 16, f"lookback:{_ext.stream_ptr(x.device)}")
+
+
+_ext.proto(_ext.HIP_PROTOS, "cme_lookback_timeout_word", "p")
+_timeout_word = None
+
+
+def _tw():
+    """The look-back give-up word: pinned host memory the kernels store to
+    (lookback.h), readable without a device synchronisation."""
+    global _timeout_word
+    if _timeout_word is None:
+        import ctypes
+
+        p = ctypes.c_void_p()
+        _ext.call_hip("cme_lookback_timeout_word", ctypes.addressof(p))
+        _timeout_word = ctypes.c_uint.from_address(p.value)
+    return _timeout_word
 
 
 def lookback_timed_out(device: torch.device | str = "cuda") -> bool:
-    """True if the last look-back launch on ``device`` hit its bounded-spin
-    limit (its result is then wrong). Reads the workspace timeout word
-    (lookback.h layout: word 0), so it synchronises."""
-    dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    t = _ws_cache.get(("lookback", idx))
-    return bool(t is not None and int(t[:4].view(torch.int32).item()) != 0)
+    """True if a look-back launch on ``device`` (since the last check) hit its
+    bounded-spin limit -- its result is wrong. Synchronises the device."""
+    torch.cuda.synchronize(torch.device(device))
+    return _tw().value != 0
 
 
-def _check_lookback(x: torch.Tensor) -> None:
-    if _ext.SYNC_CHECK and lookback_timed_out(x.device):
-        raise RuntimeError("look-back scan spin limit exceeded: result invalid")
+def check_lookback(device: torch.device | str = "cuda") -> None:
+    """Synchronise and raise if any look-back launch gave up (then clear)."""
+    if lookback_timed_out(device):
+        _tw().value = 0
+        raise RuntimeError("look-back scan spin limit exceeded: a result since the last check is invalid")
+
+
+def _check_lookback(x: torch.Tensor, before: bool = False) -> None:
+    """Called around every look-back launch. Before one: the give-up word of
+    EARLIER launches is read without a sync (it is sticky host memory) and
+    raised. After one: only under CME_SYNC_CHECK (which synchronises)."""
+    w = _tw()
+    if before:
+        if w.value != 0:
+            w.value = 0
+            raise RuntimeError("an earlier look-back scan hit its spin limit (its result was invalid)")
+    elif _ext.SYNC_CHECK:
+        check_lookback(x.device)
 
 
 def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
@@ -81,6 +113,7 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
     if x.is_cuda:
         s = _ext.stream_ptr(x.device)
         if algo == "lookback":
+            _check_lookback(x, before=True)
             _ext.call_hip("cme_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           _lookback_ws(x).data_ptr(), s)
             _check_lookback(x)
@@ -147,6 +180,7 @@ def segmented_scan(x: torch.Tensor, flags: torch.Tensor, out: torch.Tensor | Non
     mode = 0 if flags.dtype == torch.uint8 else 1
     mp = mul.data_ptr() if mul is not None else None
     if x.is_cuda:
+        _check_lookback(x, before=True)
         _ext.call_hip("cme_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n,
                       _lookback_ws(x).data_ptr(), _ext.stream_ptr(x.device))
         _check_lookback(x)
@@ -163,6 +197,7 @@ def spmv_scan_run(a: torch.Tensor, xx: torch.Tensor, flags: torch.Tensor, iters:
             segmented_scan(a, flags, out=a, mul=xx)
         return a
     assert flags.dtype == torch.int32, "bitmask flags expected"
+    _check_lookback(a, before=True)
     _ext.call_hip("cme_spmv_scan_run", a.data_ptr(), xx.data_ptr(), flags.data_ptr(), a.numel(), iters,
                   _lookback_ws(a).data_ptr(), _ext.stream_ptr(a.device))
     _check_lookback(a)

@@ -20,6 +20,26 @@
 
 using namespace cme;
 
+// The look-back give-up word: pinned, mapped host memory (lookback.h). One per
+// process; device stores reach it directly, the host reads it without a sync.
+unsigned* cme::lb_host_timeout() {
+    static unsigned* w = [] {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (unsigned*)nullptr;
+        *(volatile unsigned*)p = 0u;
+        return (unsigned*)p;
+    }();
+    return w;
+}
+
+// Host address of that word (ops/scan.py reads / clears it).
+CME_EXPORT int cme_lookback_timeout_word(void** host_word) {
+    unsigned* w = lb_host_timeout();
+    if (!w) return (int)hipErrorOutOfMemory;
+    *host_word = w;
+    return 0;
+}
+
 namespace {
 
 constexpr int kScanThreads = 256;
@@ -150,7 +170,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
                 s_prefix[parity] = T(0);
             }
         } else {
-            T pre = lb_lookback<T, false, LBD>(desc, tile, timeout);
+            T pre;
+            if constexpr (LBD < 0)
+                pre = lb_lookback_probe<T, false, -LBD>(desc, tile, timeout);
+            else if constexpr (LBD >= 100)  // tuning: window 1, s_sleep(LBD - 100) back-off
+                pre = lb_lookback<T, false, 1, LBD - 100>(desc, tile, timeout);
+            else
+                pre = lb_lookback<T, false, LBD>(desc, tile, timeout);
             if (lane == 0) {
                 lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
                 s_prefix[parity] = pre;
@@ -745,9 +771,10 @@ int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipSt
     const int tiles = (int)((n + 1024LL * kLbRows - 1) / (1024LL * kLbRows));
     static int bpc_e = persistent_blocks_per_cu(scan_lookback_kernel<T, true, kLbRows>, kScanThreads);
     static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows>, kScanThreads);
-    const int cap = kNumCU * (exclusive ? bpc_e : bpc_i);
+    const int cap = device_cu_count() * (exclusive ? bpc_e : bpc_i);
     const int grid = tiles < cap ? tiles : cap;
-    unsigned* timeout = lb_timeout_word(ws);
+    unsigned* timeout = lb_host_timeout();
+    if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
     CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
     if (exclusive)
@@ -825,41 +852,52 @@ CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1
 // co-resident grid (production); 2 one tile per block (grid = tiles, relies on
 // in-order workgroup dispatch for forward progress); 3/4 as 1/2 with a 2-wide
 // look-back window per lane; 5 persistent at half the co-resident grid;
-// 6 persistent with the look-back wave prefetching after its look-back.
+// 6 persistent with the look-back wave prefetching after its look-back;
+// 7 / 8 / 9 / 10 persistent, probe-then-window look-back (lookback.h
+// lb_lookback_probe) with a 64 x 4 / 8 / 16 / 1 window.
+template <int R, bool L, int D, bool LATE = false>
+int scan_tune_launch(const float* in, float* out, long long n, int lookback, void* ws, hipStream_t s) {
+    const long long tile = 1024LL * R;
+    const int tiles = (int)((n + tile - 1) / tile);
+    // co-resident capacity of THIS instantiation (arms differ in VGPRs)
+    int bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, R, L, D, LATE>, kScanThreads);
+    if (lookback == 5) bpc = bpc > 1 ? bpc / 2 : 1;
+    int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
+    if (lookback == 2 || lookback == 4) grid = tiles;
+    if (!lb_host_timeout()) return (int)hipErrorOutOfMemory;
+    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D, LATE>), dim3(grid), dim3(kScanThreads), 0, s, in,
+                       out, n, lb_descriptors(ws), tiles, lb_host_timeout());
+    CME_LAUNCH_STATUS();
+}
+
+template <int R>
+int scan_tune_rows(const float* in, float* out, long long n, int lookback, void* ws, hipStream_t s) {
+    switch (lookback) {
+        case 0: return scan_tune_launch<R, false, 1>(in, out, n, lookback, ws, s);
+        case 3:
+        case 4: return scan_tune_launch<R, true, 2>(in, out, n, lookback, ws, s);
+        case 6: return scan_tune_launch<R, true, 1, true>(in, out, n, lookback, ws, s);
+        case 7: return scan_tune_launch<R, true, -4>(in, out, n, lookback, ws, s);
+        case 8: return scan_tune_launch<R, true, -8>(in, out, n, lookback, ws, s);
+        case 9: return scan_tune_launch<R, true, -16>(in, out, n, lookback, ws, s);
+        case 10: return scan_tune_launch<R, true, -1>(in, out, n, lookback, ws, s);
+        case 11: return scan_tune_launch<R, true, 104>(in, out, n, lookback, ws, s);
+        case 12: return scan_tune_launch<R, true, 116>(in, out, n, lookback, ws, s);
+        case 13: return scan_tune_launch<R, true, 100>(in, out, n, lookback, ws, s);
+        default: return scan_tune_launch<R, true, 1>(in, out, n, lookback, ws, s);
+    }
+}
+
 CME_EXPORT int cme_scan_tune(const float* in, float* out, long long n, int rows, int lookback, void* ws,
                              void* stream) {
     hipStream_t s = as_stream(stream);
-    const long long tile = 1024LL * rows;
-    const int tiles = (int)((n + tile - 1) / tile);
-    int bpc = 1;
-    if (rows == 4) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 4, true>, kScanThreads);
-    else if (rows == 8) bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 8, true>, kScanThreads);
-    else bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, 16, true>, kScanThreads);
-    if (lookback == 5) bpc = bpc > 1 ? bpc / 2 : 1;
-    int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    if (lookback == 2 || lookback == 4) grid = tiles;
-    unsigned* timeout = lb_timeout_word(ws);
-    uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
-#define ST(R, L, D)                                                                                                \
-    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D>), dim3(grid), dim3(kScanThreads), 0, s, in, out, \
-                       n, desc, tiles, timeout)
-#define ST6(R)                                                                                                    \
-    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, true, 1, true>), dim3(grid), dim3(kScanThreads), 0, s, \
-                       in, out, n, desc, tiles, timeout)
-#define SR(R)                                                    \
-    if (lookback == 0) ST(R, false, 1);                          \
-    else if (lookback == 3 || lookback == 4) ST(R, true, 2);     \
-    else if (lookback == 6) ST6(R);                              \
-    else ST(R, true, 1);
-    if (rows == 4) { SR(4) }
-    else if (rows == 8) { SR(8) }
-    else if (rows == 16) { SR(16) }
-    else return (int)hipErrorInvalidValue;
-#undef SR
-#undef ST6
-#undef ST
-    CME_LAUNCH_STATUS();
+    switch (rows) {
+        case 4: return scan_tune_rows<4>(in, out, n, lookback, ws, s);
+        case 8: return scan_tune_rows<8>(in, out, n, lookback, ws, s);
+        case 16: return scan_tune_rows<16>(in, out, n, lookback, ws, s);
+        default: return (int)hipErrorInvalidValue;
+    }
 }
 
 CME_EXPORT long long cme_scan_mlevel_ws_elems(long long n) {
@@ -935,8 +973,9 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
-    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    unsigned* timeout = lb_timeout_word(ws);
+    const int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
+    unsigned* timeout = lb_host_timeout();
+    if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
     CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
 #define SEG(M, F) \
@@ -959,8 +998,9 @@ int spmv_scan_launch(float* a, const float* xx, const uint32_t* flags, long long
     constexpr long long TILE = 1024LL * ROWS;
     const int tiles = (int)((n + TILE - 1) / TILE);
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF>, kScanThreads);
-    const int grid = tiles < kNumCU * bpc ? tiles : kNumCU * bpc;
-    unsigned* timeout = lb_timeout_word(ws);
+    const int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
+    unsigned* timeout = lb_host_timeout();
+    if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
     CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
     for (int it = 0; it < iters; ++it)

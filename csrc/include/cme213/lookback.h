@@ -26,9 +26,30 @@ namespace cme {
 // when its epoch matches, so a multi-iteration driver zeroes the array ONCE
 // and gives iteration i epoch i+1 (epoch 0 never matches a zeroed word).
 enum : uint32_t { kStInvalid = 0, kStAggregate = 1, kStInclusive = 2, kStFlag = 4 };
-constexpr unsigned kSpinLimit = 1u << 22;
+// Bounded spins: ~2^18 polls (well under a second) per wait, and the timeout
+// word is STICKY -- every 256 polls a waiter re-reads it and gives up at once
+// if any tile already timed out, so a broken launch (e.g. a grid that is not
+// co-resident) ends in about one spin limit instead of one per tile.
+constexpr unsigned kSpinLimit = 1u << 18;
 
-// Workspace layout: [0, 16) timeout word (+ pad), [16, 16 + 8*tiles) descriptors.
+__device__ __forceinline__ bool lb_give_up(unsigned spins, unsigned* timeout, int lane) {
+    if (spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return true;
+    }
+    if ((spins & 255u) == 255u)
+        return __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    return false;
+}
+
+// The timeout word the kernels set lives in pinned, mapped HOST memory
+// (lb_host_timeout, scan.hip): it is never reset by a launch, so a timed-out
+// launch poisons the following ones (they give up at once) until the host
+// reads and clears it -- ops/scan.py does that before every look-back call
+// and raises, without a device synchronisation.
+unsigned* lb_host_timeout();
+
+// Workspace layout: [0, 16) unused pad, [16, 16 + 8*tiles) descriptors.
 static inline unsigned* lb_timeout_word(void* ws) { return (unsigned*)ws; }
 static inline uint64_t* lb_descriptors(void* ws) { return (uint64_t*)((char*)ws + 16); }
 static inline size_t lb_ws_bytes(long long tiles) { return 16 + (size_t)tiles * 8; }
@@ -70,7 +91,7 @@ __device__ __forceinline__ T lb_val(uint64_t d) {
 // predecessors nearer than the first terminating one must be valid. Measured
 // on MI355X (benchmarks/tune_scan.py): D = 1 is fastest -- wider windows
 // multiply the memory-side poll traffic of spinning waves.
-template <typename T, bool SEGMENTED, int D = 1>
+template <typename T, bool SEGMENTED, int D = 1, int SLEEP = 1>
 __device__ T lb_lookback(uint64_t* desc, int tile, unsigned* timeout, uint32_t epoch = 0) {
     const int lane = lane_id();
     T prefix = T(0);
@@ -105,11 +126,8 @@ __device__ T lb_lookback(uint64_t* desc, int tile, unsigned* timeout, uint32_t e
             const int k = tmask ? __builtin_ctzll(tmask) : kWave;  // nearest terminating lane
             const bool need = lane <= k;
             if (!__any(need && !lvalid)) break;
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(timeout, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+            if (lb_give_up(++spins, timeout, lane)) break;
+            __builtin_amdgcn_s_sleep(SLEEP);
         }
         const uint64_t tmask = __ballot(lterm);
         if (tmask) {
@@ -120,6 +138,32 @@ __device__ T lb_lookback(uint64_t* desc, int tile, unsigned* timeout, uint32_t e
         prefix = prefix + wave_reduce(lsum);
         base -= kWave * D;
     }
+}
+
+// Probe-then-window look-back. ONE lane polls the nearest predecessor
+// (tile-1) with s_sleep until it holds at least an aggregate -- one
+// descriptor per poll while waiting -- then the wave reads a window of 64*D
+// predecessors in one batch (D loads in flight per lane, lb_lookback). In a
+// persistent grid the tiles of a round publish their aggregates at about the
+// same time, so once the nearest one is valid the window almost always is,
+// and the walk back to the previous round's inclusive descriptors takes one
+// or two batches instead of (round position / 64) dependent 64-wide polls.
+template <typename T, bool SEGMENTED, int D>
+__device__ T lb_lookback_probe(uint64_t* desc, int tile, unsigned* timeout, uint32_t epoch = 0) {
+    const int lane = lane_id();
+    if (tile > 0) {
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = false;
+            if (lane == 0) {
+                const uint32_t hi = (uint32_t)(lb_poll(desc + tile - 1) >> 32);
+                ok = (hi >> 8) == epoch && (hi & 0xffu) != kStInvalid;
+            }
+            if (__ballot(ok)) break;
+            if (lb_give_up(spins, timeout, lane)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return lb_lookback<T, SEGMENTED, D>(desc, tile, timeout, epoch);
 }
 
 }  // namespace cme
