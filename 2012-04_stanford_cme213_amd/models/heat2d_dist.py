@@ -150,8 +150,8 @@ class DistHeat:
             raise ValueError("multi-process runs own exactly one subdomain per rank")
         if tblock not in (1, 2, 3, 4):
             raise ValueError("tblock must be 1..4")
-        if tblock > 2 and dtype == torch.float64 and torch.device(device).type == "cuda":
-            raise ValueError("tblock 3/4 (3- and 4-step passes) is fp32 only on the GPU")
+        if tblock > 3 and dtype == torch.float64 and torch.device(device).type == "cuda":
+            raise ValueError("tblock 4 (4-step passes) is fp32 only on the GPU")
         self.fma = bool(fma)
         self.variant = "fma" if self.fma else variant
         self.tblock = tblock

@@ -35,9 +35,10 @@ VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_no
             "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,
             "stream4_fma": 10}
 # variants that advance more than one timestep per launch (multi-step drivers
-# only); stream3/stream4 (3 / 4 steps per HBM pass) are fp32 only
+# only); stream4 (4 steps per HBM pass) is fp32 only, stream3 takes fp32 and
+# fp64 (one row per register block for doubles)
 MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma"}
-FP32_ONLY = {"stream3", "stream3_fma", "stream4", "stream4_fma"}
+FP32_ONLY = {"stream4", "stream4_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
 FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma"}
@@ -105,7 +106,7 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
     (nsteps-1)*B cells, e.g. into an nsteps*B-deep halo), the last one writes
     ``curr`` on every region of ``regions`` (one tuple or a list of <= 4, one
     launch). Cells of ``ext`` outside the grid's update set keep their value.
-    Bitwise equal to ``nsteps`` single steps; 3 and 4 steps are fp32 only.
+    Bitwise equal to ``nsteps`` single steps; 4 steps are fp32 only.
     On CPU it runs exactly those single steps through temporaries."""
     _check(prev, curr)
     if isinstance(regions[0], int):
@@ -129,8 +130,8 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
             heat_step(src, curr, reg, order, xcfl, ycfl, v)
         return
     f64 = prev.dtype == torch.float64
-    if f64 and nsteps > 2:
-        raise ValueError("3- and 4-step passes are fp32 only")
+    if f64 and nsteps > 3:
+        raise ValueError("4-step passes are fp32 only")
     rows, pitch = prev.shape
     flat = [int(v) for reg in regions for v in reg]
     r = (ctypes.c_int * len(flat))(*flat)

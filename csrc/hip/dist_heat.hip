@@ -707,7 +707,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if ((transport == 0 || transport == 3) && nsub != 1) return (int)hipErrorInvalidValue;
     if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
-    if (tblock < 1 || tblock > 4 || (tblock > 2 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
+    if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
     // 0 (default): border stream || interior stream; 1: border then interior
     // on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for
@@ -867,7 +867,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
 // process, neighbours' memory mapped through SubDesc.ipc). dtype 0 f32, 1 f64.
 // tblock n (1-4): n steps per exchange (nB-deep halos, `interior` shrunk by
 // nB on neighbour sides, `ext` = owned region grown by (n-1)B on neighbour
-// sides; 3 and 4 fp32 only). fma: FMA-contracted stencil.
+// sides; 4 fp32 only). fma: FMA-contracted stencil.
 CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, int nsub, int dtype, int order,
                                  double xcfl, double ycfl, int iters, int cur, int sync, int exchange_first,
                                  int tblock, int fma, int* cur_out, void* stream) {

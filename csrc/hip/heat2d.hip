@@ -769,8 +769,16 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         return variant == 4 ? launch_stream2<T, ORDER, false>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s)
                             : launch_stream2<T, ORDER, true>(prev, curr, pitch, gy, g, g, xcfl, ycfl, chunk_hint, s);
     } else if (variant >= 7 && variant <= 10) {
-        // NS = 3 (variants 7, 8) or 4 (9, 10) timesteps per launch; fp32 only
-        // (fp64 windows would not fit two waves per SIMD)
+        // NS = 3 (variants 7, 8) or 4 (9, 10) timesteps per launch; fp64:
+        // NS = 3 only, one row per register block
+        if constexpr (sizeof(T) == 8) {
+            if (variant == 7)
+                return launch_streamn_multi<T, ORDER, 3, false, 1>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                   chunk_hint, s);
+            if (variant == 8)
+                return launch_streamn_multi<T, ORDER, 3, true, 1>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                  chunk_hint, s);
+        }
         if constexpr (sizeof(T) == 4) {
             switch (variant) {
                 case 7: return launch_streamn_multi<T, ORDER, 3, false>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
@@ -914,11 +922,38 @@ CME_EXPORT int cme_heat_stepn_f32(const float* prev, float* curr, int pitch, int
                                     as_stream(stream));
 }
 
+namespace {
+// fp64 NS = 3: the streamN design with one row per register block (RB = 1):
+// three 9-row windows of 4 doubles per lane stay within two waves per SIMD.
+template <int ORDER, bool FMA>
+int stepn3_f64(const double* prev, double* curr, int pitch, int gy, const Region* gs, int n, Region e, double xcfl,
+               double ycfl, int chunk, hipStream_t s) {
+    return launch_streamn_multi<double, ORDER, 3, FMA, 1>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk, s);
+}
+template <bool FMA>
+int stepn3_f64_o(int order, const double* prev, double* curr, int pitch, int gy, const Region* gs, int n, Region e,
+                 double xcfl, double ycfl, int chunk, hipStream_t s) {
+    switch (order) {
+        case 2: return stepn3_f64<2, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk, s);
+        case 4: return stepn3_f64<4, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk, s);
+        case 8: return stepn3_f64<8, FMA>(prev, curr, pitch, gy, gs, n, e, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
 CME_EXPORT int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream) {
-    if (nsteps != 2) return (int)hipErrorInvalidValue;  // deeper passes: fp32 only
-    return cme_heat_step2_f64(prev, curr, pitch, gy, out, nout, ext, order, xcfl, ycfl, chunk, fma, stream);
+    if (nsteps == 2)
+        return cme_heat_step2_f64(prev, curr, pitch, gy, out, nout, ext, order, xcfl, ycfl, chunk, fma, stream);
+    if (nsteps != 3) return (int)hipErrorInvalidValue;  // 4-step passes: fp32 only
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    return fma ? stepn3_f64_o<true>(order, prev, curr, pitch, gy, gs, nout, e, xcfl, ycfl, chunk, as_stream(stream))
+               : stepn3_f64_o<false>(order, prev, curr, pitch, gy, gs, nout, e, xcfl, ycfl, chunk, as_stream(stream));
 }
 
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO
@@ -949,7 +984,7 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     T* bufs[2] = {a, b};
     int i = 0;
     if (variant >= 7 && variant <= 10) {
-        if (sizeof(T) != 4) return (int)hipErrorInvalidValue;
+        if (sizeof(T) != 4 && variant > 8) return (int)hipErrorInvalidValue;
         const int ns = variant <= 8 ? 3 : 4;
         for (; i + ns <= iters; i += ns) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);

@@ -66,8 +66,8 @@ def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype, fma, t
     p = SimParams(nx=333, ny=270, order=8, iters=7, sync=sync, grid_method=method, ic=5.0,
                   bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
     ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)
-    if tblock > 2 and dtype == torch.float64:
-        pytest.skip("3- and 4-step passes are fp32 only")
+    if tblock > 3 and dtype == torch.float64:
+        pytest.skip("4-step passes are fp32 only")
     sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=tblock, fma=fma)
     for d in (ref, sim):
         for s in d.subs.values():
@@ -88,6 +88,7 @@ def test_loopback_subdomains_tblock2_gpu(gpu, method, world, sync, dtype, fma, t
 @pytest.mark.parametrize("sync", [False, True])
 @pytest.mark.parametrize("tblock,fma,dtype", [(1, False, torch.float32), (2, False, torch.float64),
                                               (2, True, torch.float32), (3, True, torch.float32),
+                                              (3, True, torch.float64), (3, False, torch.float64),
                                               (4, False, torch.float32), (4, True, torch.float32)])
 def test_native_loop_loopback_transport(gpu, method, world, sync, tblock, fma, dtype):
     """The native loop (border stream || interior stream || exchange stream,

@@ -32,6 +32,7 @@ CASES_4 = [
     (2, False, 4, True, "float32"),
     (1, False, 3, True, "float32"),
     (1, True, 1, False, "float64"),
+    (2, False, 3, True, "float64"),
 ]
 
 

@@ -240,6 +240,38 @@ def test_gpu_stepn_multi_region_ext(gpu, ns):
     assert torch.equal(oc, og.cpu())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("iters", [3, 7, 8])
+def test_gpu_stream3_fp64_matches_single_steps(gpu, order, fma, iters):
+    """fp64 three-step passes (one row per register block) + tails equal the
+    CPU single steps bit for bit -- the hw5 precision (2dHeat_solution.cpp:63-84)."""
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, torch.float64)
+    g = _rand_grid(p, torch.float64, gpu)
+    c.run(iters, "fma" if fma else "naive")
+    g.run(iters, "stream3" + ("_fma" if fma else ""))
+    torch.cuda.synchronize()
+    assert np.array_equal(c.state(), g.state())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("region", [(4, 300, 4, 100), (9, 250, 17, 77), (8, 292, 8, 242)])
+@pytest.mark.parametrize("chunk", [0, 5])
+def test_gpu_stream3_fp64_subregion(gpu, region, chunk):
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float64)
+    g = _rand_grid(p, torch.float64, gpu)
+    ca, cb = c.buf[0].clone(), c.buf[0].clone()
+    ga, gb = g.buf[0].clone(), g.buf[0].clone()
+    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 6, "fma")
+    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 6, "stream3_fma", chunk)
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+
+
 def test_streamn_is_fp32_only():
     from cme213x.ops.stencil import heat_run
     p = SimParams(nx=40, ny=30, order=2)
