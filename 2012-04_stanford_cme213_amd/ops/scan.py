@@ -51,8 +51,9 @@ def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
     """Descriptor array of a look-back launch. Keyed by (device, STREAM): two
     scans enqueued on different streams must not zero / overwrite each
     other's descriptors."""
-    tiles = (x.numel() + TILE - 1) // TILE
-    return workspace(x.device, tiles * 8 + 16, f"lookback:{_ext.stream_ptr(x.device)}")
+    tiles = (x.numel() + TILE - 1) // TILE  # >= the launch's tile count (its tiles are >= TILE elements)
+    nbytes = 16 * tiles + 16 * (tiles // 64 + 1) + 64  # lookback.h lb2_ws_bytes (>= the one-level layout)
+    return workspace(x.device, nbytes, f"lookback:{_ext.stream_ptr(x.device)}")
 
 
 _ext.proto(_ext.HIP_PROTOS, "cme_lookback_timeout_word", "p")

@@ -19,7 +19,7 @@ def main():
     n = 1 << 26
     x = torch.rand(n, device="cuda")
     y = torch.empty_like(x)
-    ws = workspace(x.device, (n // 1024 + 1) * 8 + 16)
+    ws = workspace(x.device, (n // 1024 + 1) * 16 + (n // 65536 + 1) * 16 + 64)
     s = _ext.stream_ptr()
     arms = [int(a) for a in os.environ.get("CME_SCAN_ARMS", "1,0,3,6,7,8,9,10").split(",")]
     cfgs = [(r, lb) for r in (4, 8, 16) for lb in arms]
@@ -78,11 +78,22 @@ def spmv_main():
         n, p, N = BENCH_SHAPES[name]
         sol = SpmvScanSolver(generate(n, p, 100000, N, seed=1), "cuda")
         ws = _lookback_ws(sol.a)
-        for rows in (4, 8):
-            for pf in (1, 0):
+        a0 = sol.a.clone()
+        ref = None
+        from cme213x.ops.scan import _tw
+        for rows in (4, 8, 16):
+            for pf in (0, 1, 2, 3):  # bit 0 prefetch, bit 1 two-level look-back
                 f = lambda: _ext.call_hip("cme_spmv_scan_tune", sol.a.data_ptr(), sol.xx.data_ptr(),  # noqa
                                           sol.flags.data_ptr(), n, N, ws.data_ptr(), rows, pf, s)
+                sol.a.copy_(a0)
                 f()
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = sol.a.clone()
+                err = float(((sol.a - ref).abs().max() / ref.abs().max().clamp(min=1e-30)).item())
+                print(json.dumps({"matrix": name, "rows": rows, "mode": pf, "rel_err_vs_r4m0": err,
+                                  "timeout": int(_tw().value)}), flush=True)
+                _tw().value = 0
                 ts = []
                 for _ in range(5):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -92,7 +103,7 @@ def spmv_main():
                     e1.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 ms = sorted(ts)[2]
-                print(json.dumps({"matrix": name, "rows": rows, "prefetch": pf, "ms": round(ms, 4),
+                print(json.dumps({"matrix": name, "rows": rows, "mode": pf, "ms": round(ms, 4),
                                   "GBps": round(12 * n * N / ms / 1e6)}), flush=True)
 
 

@@ -46,10 +46,14 @@ constexpr int kScanThreads = 256;
 constexpr int kScanWaves = kScanThreads / kWave;
 constexpr int kScanItemsPerLane = 16;  // 4 x 16-B vectors
 constexpr int kScanTile = kScanThreads * kScanItemsPerLane;  // 4096
-// rows of 16-B vectors per lane in the production look-back scan: 8 (8192-
-// element tiles) halves the number of sequential look-back rounds vs 4;
-// benchmarks/tune_scan.py at 2^26: 0.138 ms (8) vs 0.170 (4) vs 0.142 (16)
-constexpr int kLbRows = 8;
+// Production look-back scan: 16 rows of 16-B vectors per lane (16384-element
+// tiles), the two-level look-back (lookback.h lb2_lookback) and two tiles of
+// loads in flight behind it. benchmarks/tune_scan.py at 2^26 fp32
+// (profiles/scan_tune_r2.log): 0.115 ms (4.66 TB/s) vs 0.138 for round 1's
+// one-level / 8-row / 1-deep arm and 0.103 with the look-back switched off.
+constexpr int kLbRows = 16;
+constexpr int kLbMode = 200;  // two-level look-back
+constexpr int kLbPf = 2;
 
 template <typename T>
 struct Vec4 {
@@ -92,7 +96,8 @@ __device__ __forceinline__ void store_v4(T* p, long long i, long long n, const V
 // ------------------------------------------------------------ look-back scan
 // ROWS 16-B vectors per lane (tile = 256 * 4 * ROWS elements). LOOKBACK=false
 // is a timing-only diagnostic arm (tiles scanned independently: wrong result).
-template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true, int LBD = 1, bool LATE_PF0 = false>
+template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true, int LBD = 1, bool LATE_PF0 = false,
+          int PF = 1>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                      long long n, uint64_t* desc, int tiles,
                                                                      unsigned* timeout) {
@@ -111,10 +116,18 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     // on the look-back hand-off, not on bandwidth).
     const int wid = threadIdx.x / kWave;
     Vec4<T> v[ROWS];
+    Vec4<T> vn[ROWS];  // PF = 2: tile + G, loaded one iteration ahead
     if (blockIdx.x < tiles) {
         const long long b0 = (long long)blockIdx.x * TILE + wid * WAVE_ELEMS;
 #pragma unroll
         for (int k = 0; k < ROWS; ++k) v[k] = load_v4(in, b0 + k * 256 + lane * 4, n, T(0));
+        if constexpr (PF == 2) {
+            const long long b1 = (long long)(blockIdx.x + gridDim.x) * TILE + wid * WAVE_ELEMS;
+            if (blockIdx.x + gridDim.x < tiles) {
+#pragma unroll
+                for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, b1 + k * 256 + lane * 4, n, T(0));
+            }
+        }
     }
     for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
     const long long base = (long long)tile * TILE + wid * WAVE_ELEMS;
@@ -150,19 +163,35 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
         if (w < wid) wpre = wpre + t;
         tot = tot + t;
     }
-    if (LOOKBACK && wid == 0 && lane == 0 && tile > 0) lb_publish(desc + tile, kStAggregate, lb_bits(tot));
+    constexpr bool kTwoLevel = LBD == 200;
+    if constexpr (kTwoLevel) {
+        if (wid == 0 && lane == 0) lb2_put(desc + tile, tot);  // agg[tile]
+    } else if (LOOKBACK && wid == 0 && lane == 0 && tile > 0) {
+        lb_publish(desc + tile, kStAggregate, lb_bits(tot));
+    }
     // prefetch the next tile of this block while the look-back resolves
     // (LATE_PF0: the look-back wave issues its share after the look-back, so
     // its polls do not queue behind its own prefetch in the vmcnt order)
-    Vec4<T> vn[ROWS];
+    // PF = 2 keeps two tiles of loads in flight behind the look-back: tile
+    // + G is already in vn, tile + 2G goes to vn2
+    Vec4<T> vn2[ROWS];
     const int next = tile + gridDim.x;
-    const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
-    if (next < tiles && !(LATE_PF0 && LOOKBACK && wid == 0)) {
+    const int pf_tile = PF == 2 ? next + gridDim.x : next;
+    const long long nb = (long long)pf_tile * TILE + wid * WAVE_ELEMS;
+    if (pf_tile < tiles && !(LATE_PF0 && LOOKBACK && wid == 0)) {
 #pragma unroll
-        for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
+        for (int k = 0; k < ROWS; ++k) {
+            if constexpr (PF == 2)
+                vn2[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
+            else
+                vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
+        }
     }
     if (!LOOKBACK) {
         if (threadIdx.x == 0) s_prefix[parity] = T(0);
+    } else if (kTwoLevel && wid == 0) {
+        const T pre = lb2_lookback<T>(lb2_views(desc, tiles), tile, tiles, tot, 0u, timeout);
+        if (lane == 0) s_prefix[parity] = pre;
     } else if (wid == 0) {
         if (tile == 0) {
             if (lane == 0) {
@@ -173,7 +202,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
             T pre;
             if constexpr (LBD < 0)
                 pre = lb_lookback_probe<T, false, -LBD>(desc, tile, timeout);
-            else if constexpr (LBD >= 100)  // tuning: window 1, s_sleep(LBD - 100) back-off
+            else if constexpr (LBD >= 100 && LBD < 200)  // tuning: window 1, s_sleep(LBD - 100) back-off
                 pre = lb_lookback<T, false, 1, LBD - 100>(desc, tile, timeout);
             else
                 pre = lb_lookback<T, false, LBD>(desc, tile, timeout);
@@ -197,6 +226,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     }
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) v[k] = vn[k];
+    if constexpr (PF == 2) {
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) vn[k] = vn2[k];
+    }
     }  // tile loop
 }
 
@@ -622,7 +655,7 @@ __device__ __forceinline__ SegRaw seg_load(const float* __restrict__ in, const f
 // before the look-back wait (two tiles of loads in flight per block).
 // Production: ROWS 4, no prefetch (benchmarks/tune_scan.py --spmv: prefetch
 // and 8 rows both lose to register pressure -- profiles/spmv_scan_tune.jsonl).
-template <int MODE, bool FUSED_MUL, int ROWS = 4, bool PREFETCH = false>
+template <int MODE, bool FUSED_MUL, int ROWS = 4, bool PREFETCH = false, bool LB2 = false>
 __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
                                                                float* __restrict__ out, const void* __restrict__ flags,
                                                                long long n, uint64_t* desc, int tiles,
@@ -720,15 +753,21 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
         tot_f |= tf;
     }
     const uint32_t hf = tot_f ? kStFlag : 0u;
-    if (wid == 0 && lane == 0 && tile > 0)
+    if constexpr (LB2) {
+        if (wid == 0 && lane == 0) lb2_put(desc + tile, tot_v, hf, epoch);  // agg[tile]
+    } else if (wid == 0 && lane == 0 && tile > 0) {
         lb_publish(desc + tile, kStAggregate | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
+    }
     const int next = tile + gridDim.x;
     if (PREFETCH && next < tiles) {
         const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
 #pragma unroll
         for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, nb + k * 256 + lane * 4, n);
     }
-    if (wid == 0) {
+    if (LB2 && wid == 0) {
+        const float pre = lb2_lookback<float, true>(lb2_views(desc, tiles), tile, tiles, tot_v, hf, timeout, epoch);
+        if (lane == 0) s_prefix = pre;
+    } else if (wid == 0) {
         if (tile == 0) {
             if (lane == 0) {
                 lb_publish(desc, kStInclusive | hf, __builtin_bit_cast(uint32_t, tot_v), epoch);
@@ -769,20 +808,22 @@ template <typename T>
 int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
     const int tiles = (int)((n + 1024LL * kLbRows - 1) / (1024LL * kLbRows));
-    static int bpc_e = persistent_blocks_per_cu(scan_lookback_kernel<T, true, kLbRows>, kScanThreads);
-    static int bpc_i = persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows>, kScanThreads);
+    static int bpc_e =
+        persistent_blocks_per_cu(scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf>, kScanThreads);
+    static int bpc_i =
+        persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf>, kScanThreads);
     const int cap = device_cu_count() * (exclusive ? bpc_e : bpc_i);
     const int grid = tiles < cap ? tiles : cap;
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
+    CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
     if (exclusive)
-        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows>), dim3(grid), dim3(kScanThreads), 0,
-                           s, in, out, n, desc, tiles, timeout);
+        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf>), dim3(grid),
+                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
     else
-        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows>), dim3(grid), dim3(kScanThreads), 0,
-                           s, in, out, n, desc, tiles, timeout);
+        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf>), dim3(grid),
+                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
     CME_LAUNCH_STATUS();
 }
 
@@ -843,7 +884,7 @@ CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int e
     }
 }
 
-CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1) / kScanTile) * 8 + 16; }
+CME_EXPORT long long cme_scan_ws_bytes(long long n) { return (long long)lb2_ws_bytes((n + kScanTile - 1) / kScanTile); }
 
 // Diagnostic/tuning arms of the look-back scan (f32 exclusive): rows = 4/8/16
 // vectors per lane, lookback = 0 skips the cross-tile pass (wrong results;
@@ -855,18 +896,18 @@ CME_EXPORT long long cme_scan_ws_bytes(long long n) { return ((n + kScanTile - 1
 // 6 persistent with the look-back wave prefetching after its look-back;
 // 7 / 8 / 9 / 10 persistent, probe-then-window look-back (lookback.h
 // lb_lookback_probe) with a 64 x 4 / 8 / 16 / 1 window.
-template <int R, bool L, int D, bool LATE = false>
+template <int R, bool L, int D, bool LATE = false, int PF = 1>
 int scan_tune_launch(const float* in, float* out, long long n, int lookback, void* ws, hipStream_t s) {
     const long long tile = 1024LL * R;
     const int tiles = (int)((n + tile - 1) / tile);
     // co-resident capacity of THIS instantiation (arms differ in VGPRs)
-    int bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, R, L, D, LATE>, kScanThreads);
+    int bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, R, L, D, LATE, PF>, kScanThreads);
     if (lookback == 5) bpc = bpc > 1 ? bpc / 2 : 1;
     int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
     if (lookback == 2 || lookback == 4) grid = tiles;
     if (!lb_host_timeout()) return (int)hipErrorOutOfMemory;
-    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
-    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D, LATE>), dim3(grid), dim3(kScanThreads), 0, s, in,
+    CME_TRY(hipMemsetAsync(ws, 0, D == 200 ? lb2_ws_bytes(tiles) : lb_ws_bytes(tiles), s));
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D, LATE, PF>), dim3(grid), dim3(kScanThreads), 0, s, in,
                        out, n, lb_descriptors(ws), tiles, lb_host_timeout());
     CME_LAUNCH_STATUS();
 }
@@ -885,6 +926,10 @@ int scan_tune_rows(const float* in, float* out, long long n, int lookback, void*
         case 11: return scan_tune_launch<R, true, 104>(in, out, n, lookback, ws, s);
         case 12: return scan_tune_launch<R, true, 116>(in, out, n, lookback, ws, s);
         case 13: return scan_tune_launch<R, true, 100>(in, out, n, lookback, ws, s);
+        case 14: return scan_tune_launch<R, true, 200>(in, out, n, lookback, ws, s);
+        case 15: return scan_tune_launch<R, true, 200, false, 2>(in, out, n, lookback, ws, s);
+        case 16: return scan_tune_launch<R, true, 1, false, 2>(in, out, n, lookback, ws, s);
+        case 17: return scan_tune_launch<R, false, 1, false, 2>(in, out, n, lookback, ws, s);
         default: return scan_tune_launch<R, true, 1>(in, out, n, lookback, ws, s);
     }
 }
@@ -972,14 +1017,15 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     hipStream_t s = as_stream(stream);
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
-    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true>, kScanThreads);
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, 4, false, true>, kScanThreads);
     const int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
-#define SEG(M, F) \
-    hipLaunchKernelGGL((segscan_kernel<M, F>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, flags, n, desc, tiles, timeout, 1u)
+    CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
+#define SEG(M, F)                                                                                                   \
+    hipLaunchKernelGGL((segscan_kernel<M, F, 4, false, true>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, \
+                       flags, n, desc, tiles, timeout, 1u)
     if (flag_mode == 0) {
         if (xmul) SEG(0, true); else SEG(0, false);
     } else {
@@ -992,45 +1038,63 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
 // Final-project driver: `iters` fused steps a <- segscan(a * xx) (bitmask
 // heads) with ONE descriptor memset; iteration i uses look-back epoch i+1.
 namespace {
-template <int ROWS, bool PF>
+template <int ROWS, bool PF, bool LB2 = false>
 int spmv_scan_launch(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
                      hipStream_t s) {
     constexpr long long TILE = 1024LL * ROWS;
     const int tiles = (int)((n + TILE - 1) / TILE);
-    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF>, kScanThreads);
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF, LB2>, kScanThreads);
     const int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb_ws_bytes(tiles), s));
+    CME_TRY(hipMemsetAsync(ws, 0, LB2 ? lb2_ws_bytes(tiles) : lb_ws_bytes(tiles), s));
     for (int it = 0; it < iters; ++it)
-        hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a, flags,
-                           n, desc, tiles, timeout, (uint32_t)(it + 1));
+        hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF, LB2>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a,
+                           flags, n, desc, tiles, timeout, (uint32_t)(it + 1));
     CME_LAUNCH_STATUS();
 }
 }  // namespace
 
+// Two-level look-back, 4 rows per lane; the next tile is prefetched behind
+// the look-back only when a block owns several tiles (a multi-round grid).
+// benchmarks/tune_scan.py --spmv (profiles/spmvscan_tune_r2.log), GB/s at the
+// 12 B/element model: pwtk 4821 (prefetch) / 4521, webbase-1M 4451 (no
+// prefetch) / 4157, mac_econ 2273 / 2027; round 1's one-level arm: 3931 /
+// 4257 / 2173.
 CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
                                  void* stream) {
     if (n <= 0 || iters <= 0) return 0;
-    return spmv_scan_launch<4, false>(a, xx, flags, n, iters, ws, as_stream(stream));
+    const long long tiles = (n + 4095) / 4096;
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, 4, true, true>, kScanThreads);
+    if (tiles > 2LL * device_cu_count() * bpc)
+        return spmv_scan_launch<4, true, true>(a, xx, flags, n, iters, ws, as_stream(stream));
+    return spmv_scan_launch<4, false, true>(a, xx, flags, n, iters, ws, as_stream(stream));
 }
 
-// Tuning entry (benchmarks/tune_scan.py --spmv): rows 4/8 x prefetch on/off.
+// Tuning entry (benchmarks/tune_scan.py --spmv): rows 4/8/16 x mode: bit 0
+// prefetch the next tile before the look-back, bit 1 two-level look-back.
 CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
-                                  int rows, int prefetch, void* stream) {
+                                  int rows, int mode, void* stream) {
     if (n <= 0 || iters <= 0) return 0;
     hipStream_t s = as_stream(stream);
-    if (rows == 4) return prefetch ? spmv_scan_launch<4, true>(a, xx, flags, n, iters, ws, s)
-                                   : spmv_scan_launch<4, false>(a, xx, flags, n, iters, ws, s);
-    if (rows == 8) return prefetch ? spmv_scan_launch<8, true>(a, xx, flags, n, iters, ws, s)
-                                   : spmv_scan_launch<8, false>(a, xx, flags, n, iters, ws, s);
+#define SPT(R)                                                                       \
+    switch (mode & 3) {                                                              \
+        case 0: return spmv_scan_launch<R, false, false>(a, xx, flags, n, iters, ws, s); \
+        case 1: return spmv_scan_launch<R, true, false>(a, xx, flags, n, iters, ws, s);  \
+        case 2: return spmv_scan_launch<R, false, true>(a, xx, flags, n, iters, ws, s);  \
+        default: return spmv_scan_launch<R, true, true>(a, xx, flags, n, iters, ws, s);  \
+    }
+    if (rows == 4) SPT(4)
+    if (rows == 8) SPT(8)
+    if (rows == 16) SPT(16)
+#undef SPT
     return (int)hipErrorInvalidValue;
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kLbRows>);
+CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kLbRows, true, kLbMode, false, kLbPf>);
 CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
 CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
 CME_REGISTER_KERNEL(scan_blelloch_rts_f32, 256, rts_tree_scan_kernel<float, true, 0>);
-CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true>);
+CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true, 4, false, true>);

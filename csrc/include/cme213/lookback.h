@@ -166,4 +166,126 @@ __device__ T lb_lookback_probe(uint64_t* desc, int tile, unsigned* timeout, uint
     return lb_lookback<T, SEGMENTED, D>(desc, tile, timeout, epoch);
 }
 
+// ------------------------------------------------------ two-level look-back
+// The one-level walk above advances the "inclusive frontier" by at most 64
+// tiles per dependent poll, so a launch costs about tiles/64 sequential poll
+// latencies (2^26 fp32, 8192 tiles: ~0.26 us x 128 = the measured 33 us over
+// the no-look-back arm). Two levels make that ~2 polls per tile:
+//   agg[t]   aggregate of tile t, published as soon as the tile is reduced,
+//            never changed;
+//   inc[t]   inclusive prefix through tile t, after its look-back;
+//   gagg[g]  aggregate of the 64 tiles of group g, published by the group's
+//            LAST tile as soon as the group's 64 aggregates are valid;
+//   ginc[g]  inclusive prefix through group g (the last tile's inc).
+// Tile t = 64g + j walks its own group's j predecessors (one 64-wide poll of
+// agg/inc), then groups g-1, g-2, ... 64 per poll (4096 tiles per poll), each
+// ending at the nearest inclusive entry. SEGMENTED: an aggregate carrying
+// kStFlag (a segment head inside) also ends a walk -- its value is the running
+// value at its end -- and aggregates combine as (f, v) . (f', v') =
+// (f | f', f' ? v' : v + v'). Granules: hi = (epoch << 8) | status (status 0 =
+// not yet published), lo = value bits; the arrays are zeroed once per launch
+// (or per multi-iteration run, with a new epoch per iteration). Every wait
+// depends only on aggregates published at tile start or on inclusive values
+// of strictly earlier tiles, so a co-resident grid always makes progress.
+struct Lb2 {
+    uint64_t *agg, *inc, *gagg, *ginc;
+};
+static inline size_t lb2_ws_bytes(long long tiles) { return 16 + 16 * (size_t)tiles + 16 * (size_t)((tiles + 63) / 64); }
+__host__ __device__ static inline Lb2 lb2_views(uint64_t* desc, long long tiles) {
+    const long long groups = (tiles + 63) / 64;
+    return Lb2{desc, desc + tiles, desc + 2 * tiles, desc + 2 * tiles + groups};
+}
+template <typename T>
+__device__ __forceinline__ void lb2_put(uint64_t* d, T v, uint32_t flag = 0, uint32_t epoch = 0) {
+    lb_publish(d, kStAggregate | flag, lb_bits(v), epoch);
+}
+__device__ __forceinline__ uint32_t lb2_status(uint64_t d, uint32_t epoch) {
+    const uint32_t hi = (uint32_t)(d >> 32);
+    return (hi >> 8) == epoch ? (hi & 0xffu) : 0u;
+}
+
+// One wave: lanes l < n inspect predecessor slot base - l of (a, inc).
+// Returns (via *sum) the combination of the entries nearer than the
+// nearest terminating one (a valid inc, or a flagged agg when SEGMENTED) plus
+// that entry, and whether a terminator was found. `virt0`: slots before 0 are
+// an inclusive 0 (the start of the array). `all_agg`: additionally require
+// EVERY lane's aggregate and fold them all into (*gsum, *gflag) -- the group's
+// last tile builds gagg from them.
+template <typename T, bool SEG>
+__device__ __forceinline__ bool lb2_window(const uint64_t* a, const uint64_t* inc, int base, int n, bool virt0,
+                                           bool all_agg, uint32_t epoch, T* sum, T* gsum, uint32_t* gflag,
+                                           unsigned* timeout) {
+    const int lane = lane_id();
+    for (unsigned spins = 0;; ++spins) {
+        const int idx = base - lane;
+        const bool act = lane < n && idx >= 0;
+        const bool virt = lane < n && idx < 0 && virt0;
+        const uint64_t da = act ? lb_poll((uint64_t*)a + idx) : 0;
+        const uint64_t di = act ? lb_poll((uint64_t*)inc + idx) : 0;
+        const uint32_t sa = lb2_status(da, epoch), si = lb2_status(di, epoch);
+        const bool aval = act && sa != 0u;
+        const bool aflag = SEG && aval && (sa & kStFlag);
+        const bool ival = (act && si != 0u) || virt;
+        const bool term = ival || aflag;
+        const uint64_t tm = __ballot(term);
+        const int k = tm ? __builtin_ctzll(tm) : kWave;
+        bool bad = lane < k && lane < n && !virt && !aval;
+        if (all_agg) bad = bad || (act && !aval);
+        if (!__any(bad)) {
+            // lane k contributes its inclusive value (or its flagged aggregate)
+            const bool use_inc = lane == k && act && si != 0u;
+            const T c = lane < k ? (aval ? lb_val<T>(da) : T(0)) : (lane == k && act ? lb_val<T>(use_inc ? di : da) : T(0));
+            *sum = wave_reduce(c);
+            if (all_agg) {
+                // ordered segmented fold of every aggregate (nearest first):
+                // stop at the nearest flagged one
+                const uint64_t fm = SEG ? __ballot(aflag) : 0ull;
+                const int kf = fm ? __builtin_ctzll(fm) : kWave;
+                *gsum = wave_reduce(act && lane <= kf ? lb_val<T>(da) : T(0));
+                *gflag = kf < kWave ? 1u : 0u;
+            }
+            return k < kWave;
+        }
+        if (lb_give_up(spins, timeout, lane)) {
+            *sum = T(0);
+            if (all_agg) *gsum = T(0), *gflag = 0u;
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Exclusive prefix of tile `tile` (aggregate (tot, tot_flag) already in
+// agg[]); publishes inc[tile] (and gagg / ginc for a group's last tile). For
+// SEGMENTED the returned prefix is the running value entering the tile (the
+// caller ignores it past the tile's first head). One wave.
+template <typename T, bool SEG = false>
+__device__ T lb2_lookback(Lb2 w, int tile, int tiles, T tot, uint32_t tot_flag, unsigned* timeout,
+                          uint32_t epoch = 0) {
+    const int lane = lane_id();
+    const int g = tile >> 6, j = tile & 63;
+    const bool last = j == 63 || tile == tiles - 1;
+    T prefix = T(0), gsum = T(0);
+    uint32_t gflag = 0u;
+    bool done = false;
+    if (j > 0) done = lb2_window<T, SEG>(w.agg, w.inc, tile - 1, j, false, last, epoch, &prefix, &gsum, &gflag, timeout);
+    if (last && lane == 0) {  // unblock later groups before walking on
+        const T gv = tot_flag ? tot : gsum + tot;
+        lb2_put(w.gagg + g, gv, (tot_flag | gflag) ? kStFlag : 0u, epoch);
+    }
+    for (int gb = g - 1; !done && gb >= 0; gb -= kWave) {
+        T s, gs;
+        uint32_t gf;
+        done = lb2_window<T, SEG>(w.gagg, w.ginc, gb, kWave, true, false, epoch, &s, &gs, &gf, timeout);
+        prefix = prefix + s;
+    }
+    if (lane == 0) {
+        const T incl = tot_flag ? tot : prefix + tot;
+        const uint32_t fl = tot_flag ? kStFlag : 0u;  // informational only: inc always terminates a walk
+        lb2_put(w.inc + tile, incl, fl, epoch);
+        if (last) lb2_put(w.ginc + g, incl, fl, epoch);
+    }
+    return prefix;
+}
+
 }  // namespace cme
