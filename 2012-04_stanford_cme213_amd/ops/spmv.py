@@ -265,7 +265,8 @@ def auto_group(a: CSR) -> int:
 
 def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
     """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
-    "scalar", "vector", or "auto" (vector with auto group)."""
+    "scalar", "vector", or "auto" (vector with auto group). To pick the
+    FORMAT by the matrix structure, convert once with :func:`prepare`."""
     if y is None:
         nrows = a.ell.nrows if isinstance(a, HYB) else a.nrows
         y = torch.zeros(nrows, dtype=torch.float32, device=x.device)
@@ -301,6 +302,65 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
     else:
         raise TypeError(type(a))
     return y
+
+
+# ------------------------------------------------------- format selection
+@dataclass
+class MatrixStats:
+    nrows: int
+    nnz: int
+    mean_row: float
+    max_row: int
+    cv_row: float  # coefficient of variation of the row lengths
+    ndiag: int  # occupied diagonals
+    dia_fill: float  # nnz / (ndiag * nrows)
+    ell_fill: float  # nnz / (max_row * nrows)
+
+
+def matrix_stats(a: CSR) -> MatrixStats:
+    lens = np.diff(a.rp.cpu().numpy().astype(np.int64))
+    mean = a.nnz / max(1, a.nrows)
+    mx = int(lens.max()) if lens.size else 0
+    cv = float(lens.std() / mean) if mean > 0 else 0.0
+    # occupied diagonals, counted on a sample of rows when the matrix is large
+    rows = _row_ids(a)
+    off = a.col.cpu().numpy().astype(np.int64) - rows
+    if off.size > (1 << 24):
+        off = off[np.random.default_rng(0).integers(0, off.size, 1 << 22)]
+    ndiag = int(np.unique(off).size)
+    return MatrixStats(a.nrows, a.nnz, mean, mx, cv, ndiag, a.nnz / max(1, ndiag * a.nrows),
+                       a.nnz / max(1, mx * a.nrows))
+
+
+def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
+    """Bell & Garland's decision rules (``refs/Bell SC 2009.pdf`` §3-4),
+    with thresholds set from the MI355X per-format table (profiles/spmv_r2.md):
+      * DIA  -- few diagonals, densely filled (structured stencils);
+      * ELL  -- regular rows (max row length close to the mean);
+      * HYB  -- ELL for the typical rows + COO for a heavy tail (power-law
+                rows would serialise CSR lanes on the longest row);
+      * CSR-vector (16-B aligned rows) -- everything else."""
+    st = stats or matrix_stats(a)
+    if st.ndiag <= 64 and st.dia_fill >= 0.6:
+        return "dia"
+    if st.max_row <= 64 and st.ell_fill >= 0.66:
+        return "ell"
+    if st.max_row > 8 * max(1.0, st.mean_row) or st.cv_row > 1.0:
+        return "hyb"
+    return "csr_aligned"
+
+
+def prepare(a: CSR, fmt: str = "auto", device=None):
+    """Convert ``a`` to ``fmt`` ("auto" = :func:`choose_format`) on ``device``;
+    returns (format name, matrix) ready for :func:`spmv`."""
+    if fmt == "auto":
+        fmt = choose_format(a)
+    conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_aligned": to_csr_aligned,
+            "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}
+    if fmt not in conv:
+        raise ValueError(f"unknown SpMV format {fmt!r}")
+    m = conv[fmt](a)
+    return fmt, (m.to(device) if device is not None else m)
 
 
 def bytes_per_nnz(fmt: str) -> float:

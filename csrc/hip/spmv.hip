@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void dia_kernel(int nrows, int ncols, int ndia
     __shared__ int s_off[64];
     for (int i = threadIdx.x; i < ndiag && i < 64; i += blockDim.x) s_off[i] = offsets[i];
     __syncthreads();
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // see dia4_kernel
     if (r >= nrows) return;
     float s = 0.f;
     int d = 0;
@@ -150,6 +150,50 @@ __global__ __launch_bounds__(256) void dia_kernel(int nrows, int ncols, int ndia
         s += (c >= 0 && c < ncols) ? v * xv : 0.f;
     }
     y[r] = beta == 0.f ? s : beta * y[r] + s;
+}
+
+// DIA, 4 consecutive rows per lane: the diagonals are read with 16-B loads
+// and y is written with one 16-B store (the one-row kernel above issues 4-B
+// accesses: 66 % of the copy rate on the 16M-row 5-point Laplacian with the
+// MALL defeated, benchmarks/bench_spmv.py). x is gathered per row (its lines
+// are shared by the neighbouring diagonals and rows: L1/L2 hits). Needs
+// nrows % 4 == 0 (16-B aligned diagonals); the launcher falls back otherwise.
+__global__ __launch_bounds__(256) void dia4_kernel(int nrows, int ncols, int ndiag, const int* __restrict__ offsets,
+                                                   const float* __restrict__ data, const float* __restrict__ x,
+                                                   float* __restrict__ y, float beta) {
+    __shared__ int s_off[64];
+    for (int i = threadIdx.x; i < ndiag && i < 64; i += blockDim.x) s_off[i] = offsets[i];
+    __syncthreads();
+    // XCD-aware order: each XCD gets a contiguous range of row blocks, so the
+    // x lines a diagonal offset re-reads (rows r +- off) hit that XCD's L2
+    const int r0 = (xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) * 4;
+    if (r0 >= nrows) return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int d = 0; d < ndiag; ++d) {
+        const int off = d < 64 ? s_off[d] : offsets[d];
+        const float4 v = *reinterpret_cast<const float4*>(data + (size_t)d * nrows + r0);
+        const int c = r0 + off;
+        float xv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int cj = c + j;
+            xv[j] = (cj >= 0 && cj < ncols) ? x[cj] : 0.f;
+        }
+        s.x += v.x * xv[0];
+        s.y += v.y * xv[1];
+        s.z += v.z * xv[2];
+        s.w += v.w * xv[3];
+    }
+    float4* yp = reinterpret_cast<float4*>(y + r0);
+    if (beta != 0.f) {
+        const float4 o = *yp;
+        s.x += beta * o.x;
+        s.y += beta * o.y;
+        s.z += beta * o.z;
+        s.w += beta * o.w;
+    }
+    *yp = s;
 }
 
 // COO: entries sorted by row. Each wave handles 256 consecutive entries as
@@ -234,6 +278,16 @@ CME_EXPORT int cme_spmv_ell(int nrows, int K, const int* col, const float* val, 
 
 CME_EXPORT int cme_spmv_dia(int nrows, int ncols, int ndiag, const int* offsets, const float* data, const float* x,
                             float* y, float beta, void* stream) {
+    // 4 rows per lane only when that still leaves >= 1M lanes (16 waves per
+    // SIMD): with 1M rows its 250K lanes lose to the one-row kernel (27-point
+    // Laplacian 41 vs 30 us, 5-point 11.0 vs 10.2 us; 16M-row 5-point 99 vs
+    // 117 us -- profiles/spmv_r2.md). CME_SPMV_DIA1 forces the one-row kernel.
+    static const bool one_row = getenv("CME_SPMV_DIA1") != nullptr;
+    if (nrows % 4 == 0 && nrows >= (4 << 20) && !one_row) {
+        hipLaunchKernelGGL(dia4_kernel, dim3(cdiv(nrows / 4, 256)), dim3(256), 0, as_stream(stream), nrows, ncols,
+                           ndiag, offsets, data, x, y, beta);
+        CME_LAUNCH_STATUS();
+    }
     hipLaunchKernelGGL(dia_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, as_stream(stream), nrows, ncols, ndiag,
                        offsets, data, x, y, beta);
     CME_LAUNCH_STATUS();
@@ -257,4 +311,5 @@ CME_REGISTER_KERNEL(spmv_csr_vector8, 256, csr_vector_kernel<8>);
 CME_REGISTER_KERNEL(spmv_csr_aligned4, 256, csr_vec4_kernel<4>);
 CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);
 CME_REGISTER_KERNEL(spmv_dia, 256, dia_kernel);
+CME_REGISTER_KERNEL(spmv_dia4, 256, dia4_kernel);
 CME_REGISTER_KERNEL(spmv_coo, 256, coo_kernel);
