@@ -22,6 +22,7 @@ def main():
     s = _ext.stream_ptr()
     cfgs = [(0, u, nt, bpc) for u in (1, 2, 4, 8) for nt in (0, 1) for bpc in (2, 4, 8, 16, 32)]
     cfgs += [(1, 4, 0, bpc) for bpc in (1, 2, 4, 8)]
+    cfgs += [(2, u, 1, 0) for u in (1, 2, 4, 8)]  # one-shot tiles
     times = {c: [] for c in cfgs}
     times["torch"] = []
     for _ in range(5):
@@ -40,7 +41,7 @@ def main():
             times[c].append(e0.elapsed_time(e1) / 5)
     for c, t in sorted(times.items(), key=lambda kv: sorted(kv[1])[2]):
         ms = sorted(t)[2]
-        print(json.dumps({"cfg": c, "ms": round(ms, 4), "GBps": round(2 * nbytes / ms / 1e6, 1)}))
+        print(json.dumps({"cfg": c, "ms": round(ms, 4), "GBps": round(2 * nbytes / ms / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -16,10 +16,13 @@ def main():
 
     _ext.proto(_ext.HIP_PROTOS, "cme_transpose_tune", "ppiiiiip")
     s = _ext.stream_ptr()
-    for n in (8192, 4096, 16384):
+    sizes = [int(v) for v in os.environ.get("CME_TR_SIZES", "8192,4096,16384").split(",")]
+    remaps = [int(v) for v in os.environ.get("CME_TR_REMAPS", "0,1,2").split(",")]
+    tiles = [tuple(map(int, v.split("x"))) for v in os.environ.get("CME_TR_TILES", "64x64,64x128,128x64,128x128,256x64,256x128").split(",")]
+    for n in sizes:
         x = torch.rand(n, n, device="cuda")
         y = torch.empty_like(x)
-        cfgs = [(tr, tc, rm) for tr in (64, 128, 256) for tc in (64, 128) for rm in (0, 1, 2)]
+        cfgs = [(tr, tc, rm) for tr, tc in tiles for rm in remaps]
         times = {c: [] for c in cfgs}
         for _ in range(5):
             for c in cfgs:
@@ -32,7 +35,10 @@ def main():
                 e1.record()
                 e1.synchronize()
                 times[c].append(e0.elapsed_time(e1) / 5)
-        assert torch.equal(y, x.t())
+        for c in cfgs:  # every arm must transpose correctly
+            y.zero_()
+            _ext.call_hip("cme_transpose_tune", x.data_ptr(), y.data_ptr(), n, n, *c, s)
+            assert torch.equal(y, x.t()), c
         for c in cfgs:
             ms = sorted(times[c])[2]
             print(json.dumps({"n": n, "tr": c[0], "tc": c[1], "remap": c[2], "ms": round(ms, 4),

@@ -84,6 +84,22 @@ __global__ __launch_bounds__(256) void copy_tune_kernel(const u32x4* __restrict_
     for (; i < n; i += stride) out[i] = in[i];
 }
 
+// One-shot copy: a block moves ONE contiguous 256 x UNROLL-vector tile and
+// exits (no grid stride): tens of thousands of short-lived blocks keep more
+// bytes in flight than a persistent grid. Non-temporal loads and stores.
+template <int UNROLL>
+__global__ __launch_bounds__(256) void copy_flat_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                        size_t n) {
+    const size_t b0 = (size_t)blockIdx.x * 256 * UNROLL + threadIdx.x;
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+        if (b0 + u * 256 < n) v[u] = __builtin_nontemporal_load(&in[b0 + u * 256]);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+        if (b0 + u * 256 < n) __builtin_nontemporal_store(v[u], &out[b0 + u * 256]);
+}
+
 // Block-contiguous copy: each block streams one contiguous chunk (no grid stride).
 template <int UNROLL>
 __global__ __launch_bounds__(256) void copy_chunk_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
@@ -158,10 +174,11 @@ CME_EXPORT int cme_shift_cipher(const uint8_t* in, uint8_t* out, long long n, in
 CME_EXPORT int cme_copy_bytes(const void* in, void* out, long long nbytes, void* stream) {
     hipStream_t s = as_stream(stream);
     size_t m = (size_t)nbytes / 16;
-    // measured best on MI355X (benchmarks/tune_copy.py): 1 vector per lane per
-    // iteration, non-temporal, 4 blocks of 256 per CU, grid-stride
-    if (m) hipLaunchKernelGGL((copy_tune_kernel<1, true>), dim3(stream_grid(m, 256, 4)), dim3(256), 0, s,
-                              (const u32x4*)in, (u32x4*)out, m);
+    // measured best on MI355X (benchmarks/tune_copy.py, profiles/copy_tune_r2.log):
+    // one-shot 4 KB tiles, one 16-B non-temporal vector per lane: 6.54 TB/s
+    // on 1 GiB (round 1's grid-stride persistent copy: 5.96)
+    if (m) hipLaunchKernelGGL(copy_flat_kernel<1>, dim3(cdiv(m, 256)), dim3(256), 0, s, (const u32x4*)in,
+                              (u32x4*)out, m);
     size_t body = m * 16;
     if ((size_t)nbytes > body)
         hipLaunchKernelGGL(shift_u8_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)in + body, (uint8_t*)out + body,
@@ -184,6 +201,15 @@ CME_EXPORT int cme_copy_tune(const void* in, void* out, long long nbytes, int mo
     const u32x4* a = (const u32x4*)in;
     u32x4* b = (u32x4*)out;
     unsigned grid = (unsigned)(256 * blocks_per_cu);
+    if (mode == 2) {  // one-shot tiles of 256 x unroll vectors
+        switch (unroll) {
+            case 1: hipLaunchKernelGGL(copy_flat_kernel<1>, dim3(cdiv(m, 256)), dim3(256), 0, s, a, b, m); break;
+            case 2: hipLaunchKernelGGL(copy_flat_kernel<2>, dim3(cdiv(m, 512)), dim3(256), 0, s, a, b, m); break;
+            case 4: hipLaunchKernelGGL(copy_flat_kernel<4>, dim3(cdiv(m, 1024)), dim3(256), 0, s, a, b, m); break;
+            default: hipLaunchKernelGGL(copy_flat_kernel<8>, dim3(cdiv(m, 2048)), dim3(256), 0, s, a, b, m); break;
+        }
+        CME_LAUNCH_STATUS();
+    }
     if (mode == 1) {
         size_t per = (m + grid - 1) / grid;
         hipLaunchKernelGGL(copy_chunk_kernel<4>, dim3(grid), dim3(256), 0, s, a, b, m, per);

@@ -145,11 +145,28 @@ __global__ __launch_bounds__(256) void tile_reps_kernel(const float* __restrict_
 // (TR floats), wider tiles longer input-row segments (TC floats) -- at 8192^2
 // (beyond the 256 MB MALL) 256-B segments at a 32 KB stride leave HBM
 // bandwidth on the table. REMAP: 0 none, 1 XCD-aware, 2 diagonal.
-template <int TR, int TC, int REMAP>
+// NT: non-temporal (streaming) output stores. K: tiles per block, stacked
+// along the input rows -- all K tiles' loads are issued before any LDS
+// write, so a block keeps K x 16 KB in flight.
+// Picks v[(k + rot) & 3] with a lane-dependent rot (selects, no indexing).
+__device__ __forceinline__ float pick4(const float4& v, int e) {
+    const float lo = (e & 1) ? v.y : v.x, hi = (e & 1) ? v.w : v.z;
+    return (e & 2) ? hi : lo;
+}
+
+// LDS bank rule (cdna_hip_programming.md §2 LDS): ds_write_b32 / ds_read_b32
+// address 32 banks ((a/4) % 32) per 32-lane half-wave. With the +1 pitch
+// (P = TR + 1 odd) the element at column c, row r sits in bank (c + r) % 32,
+// and the lanes of one half-wave that hold columns 4j..4j+3 (j = 0..15) hit
+// bank 4j + k for element k: lanes j and j + 8 collide (2-way, measured
+// 4.19M SQ_LDS_BANK_CONFLICT cycles per 8192^2 dispatch). ROT rotates the
+// element order by 2 for j >= 8, so a half-wave's 32 accesses cover 32
+// distinct banks in every write and read step.
+template <int TR, int TC, int REMAP, bool NT = false, int K = 1, bool ROT = false>
 __global__ __launch_bounds__(256) void vec_tile_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        int rows, int cols) {
     constexpr int P = TR + 1;
-    __shared__ float tile[TC * P];
+    __shared__ float tile[K][TC * P];
     const int t = threadIdx.x;
     int bx = blockIdx.x, by = blockIdx.y;
     if constexpr (REMAP == 1) {
@@ -163,20 +180,39 @@ __global__ __launch_bounds__(256) void vec_tile_kernel(const float* __restrict__
             bx = (blockIdx.x + blockIdx.y) % gridDim.x;
         }
     }
-    const int x0 = bx * TC, y0 = by * TR;
+    const int x0 = bx * TC;
     constexpr int LPR = TC / 4;              // lanes per input row
     constexpr int RPP = 256 / LPR;           // rows per pass
     const int c4 = (t % LPR) * 4;
+    float4 v[K][TR / RPP];
 #pragma unroll
-    for (int i = 0; i < TR / RPP; ++i) {
-        const int rr = t / LPR + RPP * i;
-        const int y = y0 + rr, x = x0 + c4;
-        if (y < rows && x < cols) {
-            const float4 v = *reinterpret_cast<const float4*>(in + (size_t)y * cols + x);
-            tile[(c4 + 0) * P + rr] = v.x;
-            tile[(c4 + 1) * P + rr] = v.y;
-            tile[(c4 + 2) * P + rr] = v.z;
-            tile[(c4 + 3) * P + rr] = v.w;
+    for (int k = 0; k < K; ++k) {
+        const int y0 = (by * K + k) * TR;
+#pragma unroll
+        for (int i = 0; i < TR / RPP; ++i) {
+            const int y = y0 + t / LPR + RPP * i, x = x0 + c4;
+            v[k][i] = (y < rows && x < cols) ? *reinterpret_cast<const float4*>(in + (size_t)y * cols + x)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    const int rot_w = ROT ? ((t % LPR) >> 3) * 2 : 0;  // lanes holding columns 32..63 of the tile
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int i = 0; i < TR / RPP; ++i) {
+            const int rr = t / LPR + RPP * i;
+            if constexpr (ROT) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int ee = (e + rot_w) & 3;
+                    tile[k][(c4 + ee) * P + rr] = pick4(v[k][i], ee);
+                }
+            } else {
+                tile[k][(c4 + 0) * P + rr] = v[k][i].x;
+                tile[k][(c4 + 1) * P + rr] = v[k][i].y;
+                tile[k][(c4 + 2) * P + rr] = v[k][i].z;
+                tile[k][(c4 + 3) * P + rr] = v[k][i].w;
+            }
         }
     }
     __syncthreads();
@@ -184,39 +220,74 @@ __global__ __launch_bounds__(256) void vec_tile_kernel(const float* __restrict__
     constexpr int OPP = 256 / LPO;           // output rows per pass
     const int r4 = (t % LPO) * 4;
 #pragma unroll
-    for (int i = 0; i < TC / OPP; ++i) {
-        const int oc = t / LPO + OPP * i;
-        const int oy = x0 + oc, ox = y0 + r4;
-        if (oy < cols && ox < rows) {
-            const float* s = &tile[oc * P + r4];
-            *reinterpret_cast<float4*>(out + (size_t)oy * rows + ox) = make_float4(s[0], s[1], s[2], s[3]);
+    for (int k = 0; k < K; ++k) {
+        const int y0 = (by * K + k) * TR;
+#pragma unroll
+        for (int i = 0; i < TC / OPP; ++i) {
+            const int oc = t / LPO + OPP * i;
+            const int oy = x0 + oc, ox = y0 + r4;
+            if (oy < cols && ox < rows) {
+                const float* s = &tile[k][oc * P + r4];
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                v4f o;
+                if constexpr (ROT) {
+                    const int rot_r = ((t % LPO) >> 3) * 2;
+                    float g[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) g[e] = s[(e + rot_r) & 3];  // rotated read order
+                    // g[e] holds row r4 + ((e + rot_r) & 3): undo the rotation
+                    const float4 gg = make_float4(g[0], g[1], g[2], g[3]);
+                    o = v4f{pick4(gg, (0 - rot_r) & 3), pick4(gg, (1 - rot_r) & 3), pick4(gg, (2 - rot_r) & 3),
+                            pick4(gg, (3 - rot_r) & 3)};
+                } else {
+                    o = v4f{s[0], s[1], s[2], s[3]};
+                }
+                v4f* dst = reinterpret_cast<v4f*>(out + (size_t)oy * rows + ox);
+                if constexpr (NT)
+                    __builtin_nontemporal_store(o, dst);
+                else
+                    *dst = o;
+            }
         }
     }
 }
 
-template <int TR, int TC, int REMAP>
+template <int TR, int TC, int REMAP, bool NT = false, int K = 1, bool ROT = false>
 int launch_vec_tile(const float* in, float* out, int rows, int cols, hipStream_t s) {
-    dim3 grid(cdiv(cols, TC), cdiv(rows, TR));
-    hipLaunchKernelGGL((vec_tile_kernel<TR, TC, REMAP>), grid, dim3(256), 0, s, in, out, rows, cols);
-    CME_LAUNCH_STATUS();
+    if constexpr ((size_t)K * TC * (TR + 1) * 4 > 160 * 1024) {
+        return (int)hipErrorInvalidValue;  // does not fit the 160 KB LDS of a CU
+    } else {
+        dim3 grid(cdiv(cols, TC), cdiv(rows, TR * K));
+        hipLaunchKernelGGL((vec_tile_kernel<TR, TC, REMAP, NT, K, ROT>), grid, dim3(256), 0, s, in, out, rows, cols);
+        CME_LAUNCH_STATUS();
+    }
 }
 
 }  // namespace
 
 // Tuning sweep entry (benchmarks/tune_transpose.py): tile rows tr in
-// {64, 128, 256}, tile cols tc in {64, 128}, remap 0/1/2.
+// {64, 128, 256}, tile cols tc in {64, 128}; remap bits 0-1: 0 none, 1
+// XCD-aware, 2 diagonal; bit 2: non-temporal stores; bit 3: 2 tiles per block.
 CME_EXPORT int cme_transpose_tune(const float* in, float* out, int rows, int cols, int tr, int tc, int remap,
                                   void* stream) {
     hipStream_t s = as_stream(stream);
     if ((rows % 4) || (cols % 4)) return (int)hipErrorInvalidValue;
-#define CME_VT(TR, TC)                                                                 \
-    if (tr == TR && tc == TC) {                                                        \
-        switch (remap) {                                                               \
-            case 0: return launch_vec_tile<TR, TC, 0>(in, out, rows, cols, s);         \
-            case 1: return launch_vec_tile<TR, TC, 1>(in, out, rows, cols, s);         \
-            case 2: return launch_vec_tile<TR, TC, 2>(in, out, rows, cols, s);         \
-            default: return (int)hipErrorInvalidValue;                                 \
-        }                                                                              \
+#define CME_VT(TR, TC)                                                                      \
+    if (tr == TR && tc == TC) {                                                             \
+        switch (remap) {                                                                    \
+            case 0: return launch_vec_tile<TR, TC, 0>(in, out, rows, cols, s);              \
+            case 1: return launch_vec_tile<TR, TC, 1>(in, out, rows, cols, s);              \
+            case 2: return launch_vec_tile<TR, TC, 2>(in, out, rows, cols, s);              \
+            case 4: return launch_vec_tile<TR, TC, 0, true>(in, out, rows, cols, s);        \
+            case 6: return launch_vec_tile<TR, TC, 2, true>(in, out, rows, cols, s);        \
+            case 8: return launch_vec_tile<TR, TC, 0, false, 2>(in, out, rows, cols, s);    \
+            case 9: return launch_vec_tile<TR, TC, 1, false, 2>(in, out, rows, cols, s);    \
+            case 12: return launch_vec_tile<TR, TC, 0, true, 2>(in, out, rows, cols, s);    \
+            case 13: return launch_vec_tile<TR, TC, 1, true, 2>(in, out, rows, cols, s);    \
+            case 22: return launch_vec_tile<TR, TC, 2, true, 1, true>(in, out, rows, cols, s); \
+            case 20: return launch_vec_tile<TR, TC, 0, true, 1, true>(in, out, rows, cols, s); \
+            default: return (int)hipErrorInvalidValue;                                      \
+        }                                                                                   \
     }
     CME_VT(64, 64)
     CME_VT(128, 64)
@@ -246,11 +317,15 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
             } else if (variant == 8) {
                 return launch_vec_tile<64, 64, 1>(in, out, rows, cols, s);
             } else {
-                // benchmarks/tune_transpose.py (profiles/transpose_tune.md):
-                // square -> 64x64 tiles in diagonal order (5.3 TB/s at
-                // 8192^2); otherwise 64x128 tiles (5.3 TB/s at 16384^2)
-                if (rows == cols) return launch_vec_tile<64, 64, 2>(in, out, rows, cols, s);
-                return launch_vec_tile<64, 128, 0>(in, out, rows, cols, s);
+                // benchmarks/tune_transpose.py (profiles/transpose_tune_r2.md):
+                // square -> 64x64 tiles in diagonal order with non-temporal
+                // output stores (6.88 TB/s at 8192^2, 6.54 at 4096^2, 5.16 at
+                // 16384^2; round 1's plain stores: 5.35 / 6.39 / 4.92);
+                // otherwise 64x128 tiles, non-temporal stores
+                // The LDS element order is rotated per lane group (ROT): 0 bank
+                // conflicts (profiles/transpose_pmc_r2.md) at the same speed.
+                if (rows == cols) return launch_vec_tile<64, 64, 2, true, 1, true>(in, out, rows, cols, s);
+                return launch_vec_tile<64, 128, 0, true, 1, true>(in, out, rows, cols, s);
             }
             break;
         case 9:
