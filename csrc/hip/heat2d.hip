@@ -406,7 +406,7 @@ struct StripN {
     static constexpr int kOut = (64 - 2 * NS) * 4;
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD = 1>
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD = 1, bool NT = false>
 struct StreamN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
@@ -497,10 +497,10 @@ struct StreamN {
                 const V4<T> o = upd<false>(w[NS - 1], (S + i) % NW, y);
                 T* d = dst + (size_t)y * pitch;
                 if constexpr (!CHECK) {
-                    if (out_lane) store4(d, o);
+                    if (out_lane) store_out(d, o);
                 } else if (out_lane) {
                     if (full_vec) {
-                        store4(d, o);
+                        store_out(d, o);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
@@ -516,6 +516,17 @@ struct StreamN {
             return true;
     }
 
+    // NT: the output rows are streamed past the caches (non-temporal)
+    __device__ __forceinline__ void store_out(T* d, const V4<T>& o) const {
+        if constexpr (NT && sizeof(T) == 4) {
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            const f32x4 ov = {o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(ov, reinterpret_cast<f32x4*>(d));
+        } else {
+            store4(d, o);
+        }
+    }
+
     __device__ __forceinline__ void run() {
         r0 = y0 - (NS - 1) * B;
 #pragma unroll
@@ -529,11 +540,11 @@ struct StreamN {
     }
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD>
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT = false>
 __device__ __forceinline__ void streamn_run(const T* src, T* dst, int pitch, int gy, int xbase, bool out_lane,
                                             bool full_vec, int y0, int y1, int xb, int xe, int xb1, int xe1, int yb1,
                                             int ye1, T xcfl, T ycfl) {
-    StreamN<T, ORDER, RB, NS, FMA, CHECK, PD> st;
+    StreamN<T, ORDER, RB, NS, FMA, CHECK, PD, NT> st;
     st.src = src;
     st.dst = dst;
     st.pitch = pitch;
@@ -554,7 +565,7 @@ __device__ __forceinline__ void streamn_run(const T* src, T* dst, int pitch, int
     st.run();
 }
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, int WPE = 1, int PD = 1>
+template <typename T, int ORDER, int RB, int NS, bool FMA, int WPE = 1, int PD = 1, bool NT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_streamn_kernel(
     const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
     int ye1, T xcfl, T ycfl) {
@@ -583,11 +594,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
                         (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
     if (inside)
-        streamn_run<T, ORDER, RB, NS, FMA, false, PD>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
-                                                  xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+        streamn_run<T, ORDER, RB, NS, FMA, false, PD, NT>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec,
+                                                          y0, y1, xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
     else
-        streamn_run<T, ORDER, RB, NS, FMA, true, PD>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec, y0, y1,
-                                                 xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+        streamn_run<T, ORDER, RB, NS, FMA, true, PD, NT>(prev + xl, curr + xl, pitch, gy, xbase, out_lane, full_vec,
+                                                         y0, y1, xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -712,13 +723,17 @@ int streamn_chunk(int strips, int H, int chunk_hint, long cap) {
     return ((chunk + RB - 1) / RB) * RB;
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int RB = (NS == 3 ? 4 : 2), int WPE = 1, int PD = 1>
+// NT (non-temporal output stores) defaults to on for NS = 4: benchmarks/
+// tune_heatn.py at 16384^2 (profiles/heat_streamn_nt_r2.log): NS=4 RB=2
+// 0.1833 vs 0.1922 ms/step; NS=3 RB=4 loses with it (0.1827 vs 0.179).
+template <typename T, int ORDER, int NS, bool FMA, int RB = (NS == 3 ? 4 : 2), int WPE = 1, int PD = 1,
+          bool NT = (NS == 4)>
 int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl,
                          T ycfl, int chunk_hint, hipStream_t s) {
     static_assert(NS >= 3 && NS <= 4, "streamN: 3 or 4 steps per pass");
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
-    static const long cap = resident_waves(heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD>, 256);
+    static const long cap = resident_waves(heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD, NT>, 256);
     S2Regions R{};
     int waves = 0;
     for (int i = 0; i < n; ++i) {
@@ -735,7 +750,7 @@ int launch_streamn_multi(const T* prev, T* curr, int pitch, int gy, const Region
         R.wave_end[k] = waves;
     }
     if (R.n == 0) return 0;
-    hipLaunchKernelGGL((heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
+    hipLaunchKernelGGL((heat_streamn_kernel<T, ORDER, RB, NS, FMA, WPE, PD, NT>), dim3(cdiv(waves, 4)), dim3(256), 0, s, prev,
                        curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
     CME_LAUNCH_STATUS();
 }
@@ -1131,6 +1146,9 @@ int tunen_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
         case 2: return launch_streamn_multi<float, 8, NS, true, RB, 1, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
         // pd 13: prefetch depth 1 with a 3-waves-per-SIMD register cap (<= 168 VGPRs)
         case 13: return launch_streamn_multi<float, 8, NS, true, RB, 3, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, s);
+        // pd 21: depth 1, non-temporal output stores
+        case 21: return launch_streamn_multi<float, 8, NS, true, RB, 1, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                                chunk, s);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -47,13 +47,17 @@ constexpr int kScanWaves = kScanThreads / kWave;
 constexpr int kScanItemsPerLane = 16;  // 4 x 16-B vectors
 constexpr int kScanTile = kScanThreads * kScanItemsPerLane;  // 4096
 // Production look-back scan: 16 rows of 16-B vectors per lane (16384-element
-// tiles), the two-level look-back (lookback.h lb2_lookback) and two tiles of
-// loads in flight behind it. benchmarks/tune_scan.py at 2^26 fp32
-// (profiles/scan_tune_r2.log): 0.115 ms (4.66 TB/s) vs 0.138 for round 1's
-// one-level / 8-row / 1-deep arm and 0.103 with the look-back switched off.
+// tiles), the two-level look-back (lookback.h lb2_lookback), two tiles of
+// loads in flight behind it and non-temporal output stores.
+// benchmarks/tune_scan.py at 2^26 fp32 (profiles/scan_tune_r2*.log): 0.0957
+// ms (5.61 TB/s) vs 0.138 for round 1's one-level / 8-row / 1-deep arm; 0.085
+// with the look-back switched off.
 constexpr int kLbRows = 16;
 constexpr int kLbMode = 200;  // two-level look-back
 constexpr int kLbPf = 2;
+// Non-temporal output stores (the scan output is written once): 0.0957 ms
+// (5.61 TB/s, 86 % of the one-shot copy) vs 0.115 with plain stores.
+constexpr bool kLbNt = true;
 
 template <typename T>
 struct Vec4 {
@@ -97,7 +101,7 @@ __device__ __forceinline__ void store_v4(T* p, long long i, long long n, const V
 // ROWS 16-B vectors per lane (tile = 256 * 4 * ROWS elements). LOOKBACK=false
 // is a timing-only diagnostic arm (tiles scanned independently: wrong result).
 template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true, int LBD = 1, bool LATE_PF0 = false,
-          int PF = 1>
+          int PF = 1, bool NTS = false>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                      long long n, uint64_t* desc, int tiles,
                                                                      unsigned* timeout) {
@@ -222,7 +226,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     for (int k = 0; k < ROWS; ++k) {
         const T q = p + ex[k];
         Vec4<T> r{q + v[k].x, q + v[k].y, q + v[k].z, q + v[k].w};
-        store_v4(out, base + k * 256 + lane * 4, n, r);
+        const long long oi = base + k * 256 + lane * 4;
+        if (NTS && oi + 3 < n) {  // write-once output: stream it past the caches
+            typedef T v4 __attribute__((ext_vector_type(4)));
+            const v4 o = {r.x, r.y, r.z, r.w};
+            __builtin_nontemporal_store(o, reinterpret_cast<v4*>(out + oi));
+        } else {
+            store_v4(out, oi, n, r);
+        }
     }
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) v[k] = vn[k];
@@ -808,10 +819,10 @@ template <typename T>
 int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
     const int tiles = (int)((n + 1024LL * kLbRows - 1) / (1024LL * kLbRows));
-    static int bpc_e =
-        persistent_blocks_per_cu(scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf>, kScanThreads);
-    static int bpc_i =
-        persistent_blocks_per_cu(scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf>, kScanThreads);
+    static int bpc_e = persistent_blocks_per_cu(
+        scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf, kLbNt>, kScanThreads);
+    static int bpc_i = persistent_blocks_per_cu(
+        scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf, kLbNt>, kScanThreads);
     const int cap = device_cu_count() * (exclusive ? bpc_e : bpc_i);
     const int grid = tiles < cap ? tiles : cap;
     unsigned* timeout = lb_host_timeout();
@@ -819,10 +830,10 @@ int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipSt
     uint64_t* desc = lb_descriptors(ws);
     CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
     if (exclusive)
-        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf>), dim3(grid),
+        hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf, kLbNt>), dim3(grid),
                            dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
     else
-        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf>), dim3(grid),
+        hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf, kLbNt>), dim3(grid),
                            dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
     CME_LAUNCH_STATUS();
 }
@@ -896,18 +907,18 @@ CME_EXPORT long long cme_scan_ws_bytes(long long n) { return (long long)lb2_ws_b
 // 6 persistent with the look-back wave prefetching after its look-back;
 // 7 / 8 / 9 / 10 persistent, probe-then-window look-back (lookback.h
 // lb_lookback_probe) with a 64 x 4 / 8 / 16 / 1 window.
-template <int R, bool L, int D, bool LATE = false, int PF = 1>
+template <int R, bool L, int D, bool LATE = false, int PF = 1, bool NTS = false>
 int scan_tune_launch(const float* in, float* out, long long n, int lookback, void* ws, hipStream_t s) {
     const long long tile = 1024LL * R;
     const int tiles = (int)((n + tile - 1) / tile);
     // co-resident capacity of THIS instantiation (arms differ in VGPRs)
-    int bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, R, L, D, LATE, PF>, kScanThreads);
+    int bpc = persistent_blocks_per_cu(scan_lookback_kernel<float, true, R, L, D, LATE, PF, NTS>, kScanThreads);
     if (lookback == 5) bpc = bpc > 1 ? bpc / 2 : 1;
     int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
     if (lookback == 2 || lookback == 4) grid = tiles;
     if (!lb_host_timeout()) return (int)hipErrorOutOfMemory;
     CME_TRY(hipMemsetAsync(ws, 0, D == 200 ? lb2_ws_bytes(tiles) : lb_ws_bytes(tiles), s));
-    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D, LATE, PF>), dim3(grid), dim3(kScanThreads), 0, s, in,
+    hipLaunchKernelGGL((scan_lookback_kernel<float, true, R, L, D, LATE, PF, NTS>), dim3(grid), dim3(kScanThreads), 0, s, in,
                        out, n, lb_descriptors(ws), tiles, lb_host_timeout());
     CME_LAUNCH_STATUS();
 }
@@ -930,6 +941,8 @@ int scan_tune_rows(const float* in, float* out, long long n, int lookback, void*
         case 15: return scan_tune_launch<R, true, 200, false, 2>(in, out, n, lookback, ws, s);
         case 16: return scan_tune_launch<R, true, 1, false, 2>(in, out, n, lookback, ws, s);
         case 17: return scan_tune_launch<R, false, 1, false, 2>(in, out, n, lookback, ws, s);
+        case 18: return scan_tune_launch<R, true, 200, false, 2, true>(in, out, n, lookback, ws, s);
+        case 19: return scan_tune_launch<R, false, 1, false, 2, true>(in, out, n, lookback, ws, s);
         default: return scan_tune_launch<R, true, 1>(in, out, n, lookback, ws, s);
     }
 }
@@ -1093,7 +1106,8 @@ CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* fla
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(scan_lookback_f32, 256, scan_lookback_kernel<float, true, kLbRows, true, kLbMode, false, kLbPf>);
+CME_REGISTER_KERNEL(scan_lookback_f32, 256,
+                    scan_lookback_kernel<float, true, kLbRows, true, kLbMode, false, kLbPf, kLbNt>);
 CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
 CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
 CME_REGISTER_KERNEL(scan_blelloch_rts_f32, 256, rts_tree_scan_kernel<float, true, 0>);
