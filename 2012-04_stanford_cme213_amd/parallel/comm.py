@@ -81,7 +81,7 @@ class TorchComm(Comm):
     def exchange(self, ops: list[P2P]) -> Pending:
         if not ops:
             return Pending()
-        if self.backend == "gloo" and any(o.tensor.is_cuda for o in ops):
+        if any(self._staged(o.tensor) for o in ops):
             return self._exchange_host_staged(ops)
         p2p = [dist.P2POp(dist.isend if o.kind == "send" else dist.irecv, o.tensor, self._global(o.peer),
                           group=self.group) for o in ops]
@@ -113,7 +113,7 @@ class TorchComm(Comm):
         return _Staged()
 
     def allreduce_(self, t, op="sum"):
-        if self.backend == "gloo" and t.is_cuda:
+        if self._staged(t):
             h = t.cpu()
             dist.all_reduce(h, _OPS[op], group=self.group)
             t.copy_(h)
@@ -121,13 +121,22 @@ class TorchComm(Comm):
         dist.all_reduce(t, _OPS[op], group=self.group)
         return t
 
+    def _staged(self, t: torch.Tensor) -> bool:
+        """gloo moves host memory only: device tensors go through host copies
+        (control plane of shared-GPU rehearsals)."""
+        return self.backend == "gloo" and t.is_cuda
+
     def allgather(self, t):
+        if self._staged(t):
+            return self.allgather(t.cpu()).to(t.device)
         flat = t.contiguous().reshape(-1)
         out = torch.empty(self.size * flat.numel(), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, flat, group=self.group)
         return out.view((self.size,) + tuple(t.shape))
 
     def reduce_scatter(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self._staged(t):
+            return self.reduce_scatter(t.cpu(), op).to(t.device)
         out = torch.empty((t.shape[0] // self.size,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.reduce_scatter_tensor(out, t.contiguous(), _OPS[op], group=self.group)
         return out
@@ -138,7 +147,7 @@ class TorchComm(Comm):
         return out
 
     def broadcast_(self, t, src=0):
-        if self.backend == "gloo" and t.is_cuda:
+        if self._staged(t):
             h = t.cpu()
             dist.broadcast(h, self._global(src), group=self.group)
             t.copy_(h)

@@ -55,16 +55,19 @@ class NativeRccl:
                       _ext.stream_ptr(t.device))
         return out
 
-    def p2p(self, ops) -> None:
-        """ops: list of (kind, tensor, peer) in one ncclGroupStart/End."""
+    def p2p(self, ops, stream: torch.cuda.Stream | None = None) -> None:
+        """ops: list of (kind, tensor, peer) in one ncclGroupStart/End, on
+        ``stream`` (default: the current stream). All tensors share a dtype."""
         n = len(ops)
+        if n == 0:
+            return
         peers = (ctypes.c_int * n)(*[o[2] for o in ops])
         sends = (ctypes.c_int * n)(*[1 if o[0] == "send" else 0 for o in ops])
         ptrs = (ctypes.c_void_p * n)(*[o[1].data_ptr() for o in ops])
         cnts = (ctypes.c_longlong * n)(*[o[1].numel() for o in ops])
         _ext.call_hip("cme_rccl_p2p", self.handle, n, ctypes.addressof(peers), ctypes.addressof(sends),
                       ctypes.addressof(ptrs), ctypes.addressof(cnts), _DT[ops[0][1].dtype],
-                      _ext.stream_ptr(ops[0][1].device))
+                      stream.cuda_stream if stream is not None else _ext.stream_ptr(ops[0][1].device))
 
     def check(self) -> None:
         """Raise if the communicator reported an asynchronous error (and

@@ -71,6 +71,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MT = 128, MK = 32, APAD = MT + 1;
 
+// Block order: xcd_remap gives each XCD a contiguous range of linear tile
+// ids; GM > 0 then walks them in groups of GM tile rows (column-major inside
+// the group), so the ~64 tiles an XCD runs at once form a GM x (64/GM) patch
+// that shares GM A panels and 64/GM B panels in its L2, instead of one tile
+// row that streams 64 different B panels.
+template <int GM>
 __global__ __launch_bounds__(256) void sgemm_mfma_kernel(int M, int N, int K, float alpha, const float* __restrict__ A,
                                                          const float* __restrict__ B, float beta,
                                                          float* __restrict__ C) {
@@ -81,7 +87,15 @@ __global__ __launch_bounds__(256) void sgemm_mfma_kernel(int M, int N, int K, fl
     const int wm = wid >> 1, wn = wid & 1;
     const unsigned nbx = N / MT, nby = M / MT;
     const unsigned lin = xcd_remap(blockIdx.x, nbx * nby);
-    const int bx = lin % nbx, by = lin / nbx;
+    int bx, by;
+    if (GM > 0 && nby % GM == 0) {
+        const unsigned per = GM * nbx, g = lin / per, w = lin % per;
+        by = g * GM + w % GM;
+        bx = w / GM;
+    } else {
+        bx = lin % nbx;
+        by = lin / nbx;
+    }
     const int r0 = by * MT, c0 = bx * MT;
 
     f32x4 ra[4], rb[4];
@@ -152,7 +166,101 @@ __global__ __launch_bounds__(256) void sgemm_mfma_kernel(int M, int N, int K, fl
             }
 }
 
+// GEMV y = alpha*A x + beta*y, row-major A[M][K] (the dense matvecs of
+// slides/Lecture20.pdf: column-block and 2-D block partitions). A is read once
+// and is the whole cost, so this is an HBM-streaming kernel, not an MFMA one:
+// G lanes share a row, each lane streams 16-B vectors of it at stride G with
+// U loads in flight, A loaded non-temporal so x (re-read by every row) stays
+// in L2; the G partial sums reduce with cross-lane shuffles. VEC=false is the
+// scalar-load variant for K*sizeof(T) % 16 != 0 or unaligned operands.
+template <typename T, int G, bool VEC>
+__global__ __launch_bounds__(256) void gemv_kernel(int M, int K, T alpha, const T* __restrict__ A,
+                                                   const T* __restrict__ x, T beta, T* __restrict__ y) {
+    constexpr int W = 16 / sizeof(T), U = 4;
+    typedef T V __attribute__((ext_vector_type(W)));
+    const int lane = threadIdx.x % G;
+    const long long row = (long long)blockIdx.x * (256 / G) + threadIdx.x / G;
+    if (row >= M) return;  // whole G-lane groups leave together: the shuffles stay within live groups
+    const T* a = A + row * K;
+    T s = 0;
+    int k0 = 0;
+    if constexpr (VEC) {
+        const V* av = reinterpret_cast<const V*>(a);
+        const V* xv = reinterpret_cast<const V*>(x);
+        const int nv = K / W;
+        int v = lane;
+        for (; v + (U - 1) * G < nv; v += U * G) {
+            V ra[U], rx[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) ra[u] = __builtin_nontemporal_load(av + v + u * G);
+#pragma unroll
+            for (int u = 0; u < U; ++u) rx[u] = xv[v + u * G];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int w = 0; w < W; ++w) s += ra[u][w] * rx[u][w];
+        }
+        for (; v < nv; v += G) {
+            const V ra = __builtin_nontemporal_load(av + v), rx = xv[v];
+#pragma unroll
+            for (int w = 0; w < W; ++w) s += ra[w] * rx[w];
+        }
+        k0 = nv * W;
+    }
+    for (int k = k0 + lane; k < K; k += G) s += a[k] * x[k];
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, G);
+    if (lane == 0) y[row] = alpha * s + (beta == T(0) ? T(0) : beta * y[row]);
+}
+
+template <typename T>
+int launch_gemv(int M, int K, T alpha, const T* A, const T* x, T beta, T* y, hipStream_t s) {
+    constexpr int W = 16 / sizeof(T);
+    const bool vec = K % W == 0 && (uintptr_t)A % 16 == 0 && (uintptr_t)x % 16 == 0;
+    // lanes per row: enough that each lane streams ~2 vectors per row, 4..64
+    const int nv = (K + W - 1) / W;
+    int G = 4;
+    while (G < 64 && 2 * G < nv) G *= 2;
+    const dim3 grid(cdiv(M, 256 / G));
+    switch (G * 2 + vec) {
+#define GV(g)                                                                                                         \
+    case 2 * g: hipLaunchKernelGGL((gemv_kernel<T, g, false>), grid, dim3(256), 0, s, M, K, alpha, A, x, beta, y); break; \
+    case 2 * g + 1: hipLaunchKernelGGL((gemv_kernel<T, g, true>), grid, dim3(256), 0, s, M, K, alpha, A, x, beta, y); break;
+        GV(4) GV(8) GV(16) GV(32) GV(64)
+#undef GV
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
+
 }  // namespace
+
+// y = alpha*A x + beta*y; dtype 0 f32, 4 f64 (codes of the CPU backend)
+CME_EXPORT int cme_gemv(int M, int K, double alpha, const void* A, const void* x, double beta, void* y, int dtype,
+                        void* stream) {
+    if (M <= 0) return 0;
+    hipStream_t s = as_stream(stream);
+    if (dtype == 0)
+        return launch_gemv<float>(M, K, (float)alpha, (const float*)A, (const float*)x, (float)beta, (float*)y, s);
+    if (dtype == 4) return launch_gemv<double>(M, K, alpha, (const double*)A, (const double*)x, beta, (double*)y, s);
+    return (int)hipErrorInvalidValue;
+}
+
+constexpr int kSgemmGroup = 8;
+
+// tuning arms of the mfma kernel (benchmarks/tune_sgemm.py): arm = group rows
+CME_EXPORT int cme_sgemm_tune(int M, int N, int K, const float* A, const float* B, float* C, int arm, void* stream) {
+    if (M % MT || N % MT || K % MK) return (int)hipErrorInvalidValue;
+    hipStream_t s = as_stream(stream);
+    const dim3 grid((M / MT) * (N / MT));
+    switch (arm) {
+#define ARM(g) case g: hipLaunchKernelGGL(sgemm_mfma_kernel<g>, grid, dim3(256), 0, s, M, N, K, 1.f, A, B, 0.f, C); break;
+        ARM(0) ARM(1) ARM(2) ARM(4) ARM(8) ARM(16)
+#undef ARM
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
 
 // variant: 0 naive, 1 lds, 2 mfma (falls back to lds when shapes don't tile)
 CME_EXPORT int cme_sgemm(int M, int N, int K, float alpha, const float* A, const float* B, float beta, float* C,
@@ -169,8 +277,8 @@ CME_EXPORT int cme_sgemm(int M, int N, int K, float alpha, const float* A, const
                                beta, C);
             break;
         case 2:
-            hipLaunchKernelGGL(sgemm_mfma_kernel, dim3((M / MT) * (N / MT)), dim3(256), 0, s, M, N, K, alpha, A, B,
-                               beta, C);
+            hipLaunchKernelGGL(sgemm_mfma_kernel<kSgemmGroup>, dim3((M / MT) * (N / MT)), dim3(256), 0, s, M, N, K,
+                               alpha, A, B, beta, C);
             break;
         default: return (int)hipErrorInvalidValue;
     }
@@ -180,4 +288,4 @@ CME_EXPORT int cme_sgemm(int M, int N, int K, float alpha, const float* A, const
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(sgemm_naive, 256, sgemm_naive_kernel);
 CME_REGISTER_KERNEL(sgemm_lds, 256, sgemm_lds_kernel);
-CME_REGISTER_KERNEL(sgemm_mfma, 256, sgemm_mfma_kernel);
+CME_REGISTER_KERNEL(sgemm_mfma, 256, sgemm_mfma_kernel<kSgemmGroup>);

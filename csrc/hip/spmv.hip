@@ -239,7 +239,41 @@ __global__ void scale_kernel(float* y, int n, float beta) {
     if (i < n) y[i] = beta == 0.f ? 0.f : beta * y[i];
 }
 
+// Distributed SpMV halo pieces (models/dist_spmv.py). Send side: the x
+// entries each peer needs, packed back to back in peer order (one launch for
+// all peers). Receive side: after the interior product y = A_int x_local, the
+// compact boundary rows add their off-rank columns from the received halo.
+__global__ void gather_kernel(const float* __restrict__ x, const int* __restrict__ idx, float* __restrict__ out,
+                              int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = x[idx[i]];
+}
+
+__global__ void halo_csr_kernel(int nb, const int* __restrict__ rows, const int* __restrict__ rp,
+                                const int* __restrict__ col, const float* __restrict__ val,
+                                const float* __restrict__ h, float* __restrict__ y) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    float s = 0.f;
+    for (int j = rp[b]; j < rp[b + 1]; ++j) s += val[j] * h[col[j]];
+    y[rows[b]] += s;  // rows are distinct: no atomics
+}
+
 }  // namespace
+
+CME_EXPORT int cme_gather_f32(int n, const float* x, const int* idx, float* out, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(gather_kernel, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream), x, idx, out, n);
+    CME_LAUNCH_STATUS();
+}
+
+CME_EXPORT int cme_spmv_halo(int nb, const int* rows, const int* rp, const int* col, const float* val, const float* h,
+                             float* y, void* stream) {
+    if (nb <= 0) return 0;
+    hipLaunchKernelGGL(halo_csr_kernel, dim3(cdiv(nb, 256)), dim3(256), 0, as_stream(stream), nb, rows, rp, col, val,
+                       h, y);
+    CME_LAUNCH_STATUS();
+}
 
 // y = A x (+ beta y). group: 1 scalar, else lanes per row (2..64).
 CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const float* val, const float* x, float* y,

@@ -46,6 +46,8 @@ def test_dist_spmv_bench_cpu(mode):
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
     assert rec["n_gpus"] == 3 and rec["max_abs_err"] < 1e-4
+    if mode == "halo":  # 64x64 grid in 3 row blocks: neighbours only, about one grid row each way
+        assert rec["max_peers_per_rank"] == 2 and rec["max_halo_values_per_rank"] <= 2 * 64 + 2
 
 
 def _launch_gpu(nproc, extra):

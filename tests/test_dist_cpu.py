@@ -132,6 +132,34 @@ def test_row_partitioned_spmv_gloo(mode):
         np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
 
 
+def _banded_halo_rank(rank, world):
+    import cme213x
+    from cme213x.models.dist_spmv import RowPartitionedSpMV
+    from cme213x.ops.spmv import laplacian, spmv
+    from cme213x.parallel.comm import TorchComm
+
+    n = 40
+    a = laplacian("5pt", n)
+    x = torch.from_numpy(np.random.default_rng(1).standard_normal(a.ncols).astype(np.float32))
+    op = RowPartitionedSpMV(a, TorchComm(), "cpu", mode="halo")
+    ys = [op(op.local_slice(x)).clone() for _ in range(3)]  # persistent buffers reused across calls
+    ref = spmv(a, x).numpy()[op.lo:op.hi]
+    return (rank, op.halo_volume, op.recv_peers, op.send_peers, [y.numpy() for y in ys], ref)
+
+
+def test_row_partitioned_spmv_neighbour_only():
+    """5-pt Laplacian, 6 ranks of grid rows: every rank talks to its row
+    neighbours only and moves exactly one grid row of x each way (no padded
+    all-to-all: the volume is the halo, not P x max halo)."""
+    world, n = 6, 40
+    for rank, (sent, recvd, peers), rp, sp, ys, ref in run_ranks(_banded_halo_rank, world):
+        want = [q for q in (rank - 1, rank + 1) if 0 <= q < world]
+        assert rp == want and sp == want
+        assert sent == recvd <= 2 * n + 2 and peers == len(want)
+        for y in ys:
+            np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
+
+
 def _dense_matvec_rank(rank, world):
     import cme213x
     from cme213x.models.dist_spmv import block2d_matvec, colwise_matvec

@@ -109,3 +109,45 @@ def test_ipc_two_processes_one_gpu(gpu):
 @pytest.mark.timeout(300)
 def test_ipc_four_processes_one_gpu(gpu):
     _check(4, CASES_4)
+
+
+def _spmv_rank(rank, world):
+    import torch
+
+    import cme213x  # noqa: F401
+    from cme213x.models.dist_spmv import RowPartitionedSpMV, colwise_matvec
+    from cme213x.ops.spmv import laplacian, random_csr, spmv
+    from cme213x.parallel.comm import TorchComm
+
+    torch.cuda.set_device(0)
+    comm = TorchComm()
+    out = []
+    for a in (laplacian("5pt", 150), random_csr(4000, 4000, 9, seed=5)):
+        x = torch.from_numpy(np.random.default_rng(2).standard_normal(a.ncols).astype(np.float32))
+        op = RowPartitionedSpMV(a, comm, "cuda:0", mode="halo")
+        y1 = op(op.local_slice(x).cuda()).cpu()
+        y2 = op(op.local_slice(x).cuda()).cpu()
+        out.append((y1.numpy(), y2.numpy(), spmv(a, x).numpy()[op.lo:op.hi]))
+    # column-block dense matvec: framework GEMV on the GPU, gloo reduce-scatter
+    n = 96 * world
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(n, n, generator=g)
+    xv = torch.randn(n, generator=g)
+    nb = n // world
+    part = colwise_matvec(comm, A[:, rank * nb:(rank + 1) * nb].contiguous().cuda(),
+                          xv[rank * nb:(rank + 1) * nb].cuda().contiguous())
+    ref = (A.double() @ xv.double()).float()[rank * nb:(rank + 1) * nb]
+    return out, part.cpu().numpy(), ref.numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_spmv_processes_one_gpu(gpu, world):
+    """Row-partitioned SpMV with the HIP pack (gather) and boundary kernels,
+    one process per rank on cuda:0, neighbour-only halo over gloo."""
+    for out, part, ref in run_ranks(_spmv_rank, world, (), timeout=240):
+        for y1, y2, want in out:
+            np.testing.assert_allclose(y1, want, rtol=1e-5, atol=1e-5)
+            np.testing.assert_array_equal(y1, y2)
+        np.testing.assert_allclose(part, ref, rtol=1e-4, atol=1e-3)

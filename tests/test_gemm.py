@@ -1,7 +1,7 @@
 import pytest
 import torch
 
-from cme213x.ops.gemm import sgemm
+from cme213x.ops.gemm import gemv, sgemm
 
 
 def test_sgemm_cpu():
@@ -29,3 +29,33 @@ def test_sgemm_mfma_asymmetric_identity(gpu):
     B = torch.arange(n * n, dtype=torch.float32).view(n, n) / 1000.0
     out = sgemm(A.to(gpu), B.to(gpu), variant="mfma").cpu()
     assert torch.equal(out, B)
+
+
+GEMV_SHAPES = [(1, 1), (7, 3), (64, 64), (300, 1001), (1000, 4096), (33, 20000), (4099, 130)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_gemv_cpu(dtype):
+    for M, K in GEMV_SHAPES[:5]:
+        A, x, y = torch.randn(M, K, dtype=dtype), torch.randn(K, dtype=dtype), torch.randn(M, dtype=dtype)
+        ref = 1.5 * (A.double() @ x.double()) - 0.5 * y.double()
+        out = gemv(A, x, y.clone(), 1.5, -0.5)
+        tol = 1e-4 if dtype == torch.float32 else 1e-10
+        torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol * max(1.0, K ** 0.5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("shape", GEMV_SHAPES)
+def test_gemv_gpu(gpu, dtype, shape):
+    M, K = shape
+    A, x, y = torch.randn(M, K, dtype=dtype), torch.randn(K, dtype=dtype), torch.randn(M, dtype=dtype)
+    ref = 2.0 * (A.double() @ x.double()) + 0.25 * y.double()
+    out = gemv(A.to(gpu), x.to(gpu), y.to(gpu), 2.0, 0.25).cpu()
+    tol = 1e-4 if dtype == torch.float32 else 1e-10
+    torch.testing.assert_close(out.double(), ref, rtol=tol, atol=tol * max(1.0, K ** 0.5))
+    # unaligned operands take the scalar-load kernel
+    buf = torch.randn(M * K + 1, dtype=dtype, device=gpu)
+    Au = buf[1:].view(M, K)
+    out2 = gemv(Au, x.to(gpu)).cpu()
+    torch.testing.assert_close(out2.double(), Au.cpu().double() @ x.double(), rtol=tol, atol=tol * max(1.0, K ** 0.5))
