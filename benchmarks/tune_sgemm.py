@@ -25,7 +25,7 @@ def main():
     from cme213x import _ext
     from cme213x.ops.gemm import sgemm
 
-    _ext.proto(_ext.HIP_PROTOS, "cme_sgemm_tune", "iiippppip")
+    _ext.proto(_ext.HIP_PROTOS, "cme_sgemm_tune", "iiipppip")
     arms = args.arms if args.arms is not None else [int(a) for a in os.environ.get("CME_SGEMM_ARMS", "0 8").split()]
 
     def t_ms(fn):

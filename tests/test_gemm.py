@@ -11,7 +11,8 @@ def test_sgemm_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(256, 384, 512), (128, 128, 32), (100, 70, 33), (512, 256, 1024)])
+@pytest.mark.parametrize("shape", [(256, 384, 512), (128, 128, 32), (100, 70, 33), (512, 256, 1024), (256, 256, 32),
+                                   (768, 512, 96), (1024, 1024, 2048), (4096, 4096, 64)])
 @pytest.mark.parametrize("variant", ["naive", "lds", "mfma"])
 def test_sgemm_gpu(gpu, shape, variant):
     M, N, K = shape
@@ -22,12 +23,15 @@ def test_sgemm_gpu(gpu, shape, variant):
 
 
 @pytest.mark.gpu
-def test_sgemm_mfma_asymmetric_identity(gpu):
+@pytest.mark.parametrize("n", [128, 512, 4096])
+def test_sgemm_mfma_asymmetric_identity(gpu, n):
     # A = I with an asymmetric B catches a transposed C/D register map
-    n = 128
+    # (n <= 512: the 128x128 kernel; 4096 fills the CUs with 256x256 blocks)
     A = torch.eye(n)
     B = torch.arange(n * n, dtype=torch.float32).view(n, n) / 1000.0
     out = sgemm(A.to(gpu), B.to(gpu), variant="mfma").cpu()
+    assert torch.equal(out, B)
+    out = sgemm(B.to(gpu), A.to(gpu), variant="mfma").cpu()
     assert torch.equal(out, B)
 
 

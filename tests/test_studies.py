@@ -69,7 +69,7 @@ def test_occupancy_report(gpu):
 
     rows = kernel_report()
     names = {r["kernel"] for r in rows}
-    assert {"heat_stream2_f32_o8", "sgemm_mfma", "scan_rts_scan_f32", "segscan_wave"} <= names
+    assert {"heat_stream2_f32_o8", "sgemm_mfma256", "scan_rts_scan_f32", "segscan_wave"} <= names
     for r in rows:
         assert r["blocks_per_cu"] >= 1, r
         assert 0 < r["vgprs"] <= 512, r
