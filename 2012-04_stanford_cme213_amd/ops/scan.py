@@ -18,12 +18,12 @@ import torch
 
 from .. import _ext
 
-_ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_scan", "ppqiipup")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_rts", "ppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_mlevel", "ppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_scan_tree", "ppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_reduce", "pqiiippp")
-_ext.proto(_ext.HIP_PROTOS, "cme_segscan", "ppppiqpp")
+_ext.proto(_ext.HIP_PROTOS, "cme_segscan", "ppppiqpup")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_run", "pppqipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_scan", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_reduce", "pqiip")
@@ -47,13 +47,45 @@ def workspace(device: torch.device, nbytes: int, key: str = "lookback") -> torch
     return t
 
 
-def _lookback_ws(x: torch.Tensor) -> torch.Tensor:
-    """Descriptor array of a look-back launch. Keyed by (device, STREAM): two
-    scans enqueued on different streams must not zero / overwrite each
-    other's descriptors."""
+_epochs: dict = {}
+_EPOCH_LIMIT = 1 << 24  # lookback.h: status word = (epoch << 8) | bits, 32 bits
+
+
+def _lookback_ws(x: torch.Tensor) -> tuple[torch.Tensor, int]:
+    """Descriptor array of a look-back launch and the epoch to run it with.
+    Keyed by (device, STREAM): two scans enqueued on different streams must
+    not overwrite each other's descriptors. The array is zeroed once when it
+    is (re)allocated; every launch then gets the next epoch, so stale
+    descriptors of earlier launches never match and no per-launch memset is
+    needed. Under stream capture the epoch is 0 (the native side zeroes the
+    array inside the graph), because a replayed graph repeats its arguments."""
     tiles = (x.numel() + TILE - 1) // TILE  # >= the launch's tile count (its tiles are >= TILE elements)
     nbytes = 16 * tiles + 16 * (tiles // 64 + 1) + 64  # lookback.h lb2_ws_bytes (>= the one-level layout)
-    return workspace(x.device, nbytes, f"lookback:{_ext.stream_ptr(x.device)}")
+    k = (f"lookback:{_ext.stream_ptr(x.device)}", x.device.index)
+    t = _ws_cache.get(k)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=x.device)
+        _ws_cache[k] = t
+        _epochs[k] = 0
+    if torch.cuda.is_current_stream_capturing():
+        # the graph zeroes the array at replay and writes epoch-0 words, which
+        # later epochs (>= 1) ignore; the count is NOT restarted: before a
+        # replay, words of the earlier epochs are still there
+        return t, 0
+    e = _epochs[k] + 1
+    if e >= _EPOCH_LIMIT:
+        t.zero_()
+        e = 1
+    _epochs[k] = e
+    return t, e
+
+
+def _run_ws(x: torch.Tensor) -> torch.Tensor:
+    """Descriptors for launches that zero them natively and number their own
+    epochs (spmv_scan_run, tuning arms): kept apart from :func:`_lookback_ws`,
+    whose epoch count their words would otherwise collide with."""
+    tiles = (x.numel() + TILE - 1) // TILE
+    return workspace(x.device, 16 * tiles + 16 * (tiles // 64 + 1) + 64, f"lookback-run:{_ext.stream_ptr(x.device)}")
 
 
 _ext.proto(_ext.HIP_PROTOS, "cme_lookback_timeout_word", "p")
@@ -101,9 +133,12 @@ def _check_lookback(x: torch.Tensor, before: bool = False) -> None:
 
 
 def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = None,
-         algo: str = "rts") -> torch.Tensor:
+         algo: str = "auto") -> torch.Tensor:
     """Prefix sum of a 1-D contiguous float32/int32/uint32 tensor.
-    algo: "lookback" (single pass), "rts" (reduce-then-scan with DPP wave
+    algo: "auto" ("lookback" for integers, whose sums are exact in any order;
+    "rts" for float32, whose fixed summation tree is bitwise reproducible --
+    look-back's float prefixes depend on which predecessor had published its
+    inclusive value), "lookback" (single pass), "rts" (reduce-then-scan with DPP wave
     scans, deterministic), "blelloch" / "hillis" (reduce-then-scan whose block
     level is the lecture's LDS tree algorithm), "blelloch_mlevel" /
     "hillis_mlevel" (the recursive scan-then-add of my-refs/scan.pdf Fig. 5)."""
@@ -111,12 +146,15 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
         x = x.contiguous()
     out = torch.empty_like(x) if out is None else out
     n = x.numel()
+    if algo == "auto":
+        algo = "rts" if x.dtype == torch.float32 else "lookback"
     if x.is_cuda:
         s = _ext.stream_ptr(x.device)
         if algo == "lookback":
             _check_lookback(x, before=True)
+            ws, epoch = _lookback_ws(x)
             _ext.call_hip("cme_scan", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
-                          _lookback_ws(x).data_ptr(), s)
+                          ws.data_ptr(), epoch, s)
             _check_lookback(x)
         elif algo == "rts":
             _ext.call_hip("cme_scan_rts", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
@@ -182,8 +220,9 @@ def segmented_scan(x: torch.Tensor, flags: torch.Tensor, out: torch.Tensor | Non
     mp = mul.data_ptr() if mul is not None else None
     if x.is_cuda:
         _check_lookback(x, before=True)
-        _ext.call_hip("cme_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n,
-                      _lookback_ws(x).data_ptr(), _ext.stream_ptr(x.device))
+        ws, epoch = _lookback_ws(x)
+        _ext.call_hip("cme_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n, ws.data_ptr(),
+                      epoch, _ext.stream_ptr(x.device))
         _check_lookback(x)
     else:
         _ext.call_cpu("cme_cpu_segscan", x.data_ptr(), mp, out.data_ptr(), flags.data_ptr(), mode, n)
@@ -200,6 +239,6 @@ def spmv_scan_run(a: torch.Tensor, xx: torch.Tensor, flags: torch.Tensor, iters:
     assert flags.dtype == torch.int32, "bitmask flags expected"
     _check_lookback(a, before=True)
     _ext.call_hip("cme_spmv_scan_run", a.data_ptr(), xx.data_ptr(), flags.data_ptr(), a.numel(), iters,
-                  _lookback_ws(a).data_ptr(), _ext.stream_ptr(a.device))
+                  _run_ws(a).data_ptr(), _ext.stream_ptr(a.device))
     _check_lookback(a)
     return a

@@ -73,8 +73,9 @@ def main():
         emit(bench="scan", algo="torch.cumsum", n=n, ms=ms, GBps=8 * n / ms / 1e6)
         xi = torch.randint(0, 100, (n,), device=dev, dtype=torch.int32)
         yi = torch.empty_like(xi)
-        ms = timeit(lambda: sc.scan(xi, True, yi))
-        emit(bench="scan", algo="lookback-int32", n=n, ms=ms, GBps=8 * n / ms / 1e6)
+        for algo in ("lookback", "rts"):
+            ms = timeit(lambda: sc.scan(xi, True, yi, algo))
+            emit(bench="scan", algo=f"{algo}-int32", n=n, ms=ms, GBps=8 * n / ms / 1e6)
         for algo in ("vector", "tree"):
             ms = timeit(lambda: sc.reduce(x, "sum", algo))
             emit(bench="reduce", algo=algo, n=n, ms=ms, GBps=4 * n / ms / 1e6)

@@ -70,14 +70,14 @@ def spmv_main():
     import cme213x
     from cme213x import _ext
     from cme213x.models.spmv_scan import BENCH_SHAPES, SpmvScanSolver, generate
-    from cme213x.ops.scan import _lookback_ws
+    from cme213x.ops.scan import _run_ws
 
     _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_tune", "pppqipiip")
     s = _ext.stream_ptr()
     for name in ("pwtk", "webbase-1M", "mac_econ_fwd500"):
         n, p, N = BENCH_SHAPES[name]
         sol = SpmvScanSolver(generate(n, p, 100000, N, seed=1), "cuda")
-        ws = _lookback_ws(sol.a)
+        ws = _run_ws(sol.a)
         a0 = sol.a.clone()
         ref = None
         from cme213x.ops.scan import _tw

@@ -104,7 +104,7 @@ template <typename T, bool EXCLUSIVE, int ROWS = 4, bool LOOKBACK = true, int LB
           int PF = 1, bool NTS = false>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                      long long n, uint64_t* desc, int tiles,
-                                                                     unsigned* timeout) {
+                                                                     unsigned* timeout, uint32_t epoch = 0) {
     constexpr int TILE = kScanThreads * 4 * ROWS;
     constexpr int WAVE_ELEMS = kWave * 4 * ROWS;
     __shared__ T s_wtot[2][kScanWaves];
@@ -169,9 +169,9 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     }
     constexpr bool kTwoLevel = LBD == 200;
     if constexpr (kTwoLevel) {
-        if (wid == 0 && lane == 0) lb2_put(desc + tile, tot);  // agg[tile]
+        if (wid == 0 && lane == 0) lb2_put(desc + tile, tot, 0u, epoch);  // agg[tile]
     } else if (LOOKBACK && wid == 0 && lane == 0 && tile > 0) {
-        lb_publish(desc + tile, kStAggregate, lb_bits(tot));
+        lb_publish(desc + tile, kStAggregate, lb_bits(tot), epoch);
     }
     // prefetch the next tile of this block while the look-back resolves
     // (LATE_PF0: the look-back wave issues its share after the look-back, so
@@ -194,24 +194,24 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
     if (!LOOKBACK) {
         if (threadIdx.x == 0) s_prefix[parity] = T(0);
     } else if (kTwoLevel && wid == 0) {
-        const T pre = lb2_lookback<T>(lb2_views(desc, tiles), tile, tiles, tot, 0u, timeout);
+        const T pre = lb2_lookback<T>(lb2_views(desc, tiles), tile, tiles, tot, 0u, timeout, epoch);
         if (lane == 0) s_prefix[parity] = pre;
     } else if (wid == 0) {
         if (tile == 0) {
             if (lane == 0) {
-                lb_publish(desc, kStInclusive, lb_bits(tot));
+                lb_publish(desc, kStInclusive, lb_bits(tot), epoch);
                 s_prefix[parity] = T(0);
             }
         } else {
             T pre;
             if constexpr (LBD < 0)
-                pre = lb_lookback_probe<T, false, -LBD>(desc, tile, timeout);
+                pre = lb_lookback_probe<T, false, -LBD>(desc, tile, timeout, epoch);
             else if constexpr (LBD >= 100 && LBD < 200)  // tuning: window 1, s_sleep(LBD - 100) back-off
-                pre = lb_lookback<T, false, 1, LBD - 100>(desc, tile, timeout);
+                pre = lb_lookback<T, false, 1, LBD - 100>(desc, tile, timeout, epoch);
             else
-                pre = lb_lookback<T, false, LBD>(desc, tile, timeout);
+                pre = lb_lookback<T, false, LBD>(desc, tile, timeout, epoch);
             if (lane == 0) {
-                lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot));
+                lb_publish(desc + tile, kStInclusive, lb_bits(pre + tot), epoch);
                 s_prefix[parity] = pre;
             }
         }
@@ -815,8 +815,11 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     }  // tile loop
 }
 
+// epoch 0: zero the descriptors first (one memset); epoch e > 0: the caller
+// zeroed `ws` once and gives every launch a new epoch (stale descriptors of
+// earlier launches never match), so repeated scans skip the memset.
 template <typename T>
-int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s) {
+int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipStream_t s, uint32_t epoch) {
     if (n <= 0) return 0;
     const int tiles = (int)((n + 1024LL * kLbRows - 1) / (1024LL * kLbRows));
     static int bpc_e = persistent_blocks_per_cu(
@@ -828,13 +831,14 @@ int launch_scan(const T* in, T* out, long long n, int exclusive, void* ws, hipSt
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
+    if (epoch == 0) CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
+    if (epoch >= (1u << 24)) return (int)hipErrorInvalidValue;
     if (exclusive)
         hipLaunchKernelGGL((scan_lookback_kernel<T, true, kLbRows, true, kLbMode, false, kLbPf, kLbNt>), dim3(grid),
-                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
+                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout, epoch);
     else
         hipLaunchKernelGGL((scan_lookback_kernel<T, false, kLbRows, true, kLbMode, false, kLbPf, kLbNt>), dim3(grid),
-                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout);
+                           dim3(kScanThreads), 0, s, in, out, n, desc, tiles, timeout, epoch);
     CME_LAUNCH_STATUS();
 }
 
@@ -885,12 +889,14 @@ CME_EXPORT int cme_scan_tree(const void* in, void* out, long long n, int dtype, 
 }
 
 // dtype: 0 f32, 1 i32, 2 u32. ws: >= 8*ceil(n/4096) + 16 bytes.
-CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream) {
+// epoch: see launch_scan (0 = zero the workspace here)
+CME_EXPORT int cme_scan(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, unsigned epoch,
+                        void* stream) {
     hipStream_t s = as_stream(stream);
     switch (dtype) {
-        case 0: return launch_scan<float>((const float*)in, (float*)out, n, exclusive, ws, s);
-        case 1: return launch_scan<int>((const int*)in, (int*)out, n, exclusive, ws, s);
-        case 2: return launch_scan<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, exclusive, ws, s);
+        case 0: return launch_scan<float>((const float*)in, (float*)out, n, exclusive, ws, s, epoch);
+        case 1: return launch_scan<int>((const int*)in, (int*)out, n, exclusive, ws, s, epoch);
+        case 2: return launch_scan<uint32_t>((const uint32_t*)in, (uint32_t*)out, n, exclusive, ws, s, epoch);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -1026,7 +1032,7 @@ CME_EXPORT int cme_reduce(const void* in, long long n, int dtype, int op, int al
 // Segmented inclusive scan (float add). flag_mode 0: uint8 per element;
 // 1: bitmask words. xmul != null fuses in[i]*xmul[i] (final-project step).
 CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const void* flags, int flag_mode,
-                           long long n, void* ws, void* stream) {
+                           long long n, void* ws, unsigned epoch, void* stream) {
     hipStream_t s = as_stream(stream);
     if (n <= 0) return 0;
     const int tiles = (int)((n + kScanTile - 1) / kScanTile);
@@ -1035,10 +1041,12 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
+    if (epoch == 0) CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(tiles), s));
+    if (epoch >= (1u << 24)) return (int)hipErrorInvalidValue;
+    const uint32_t ep = epoch ? epoch : 1u;
 #define SEG(M, F)                                                                                                   \
     hipLaunchKernelGGL((segscan_kernel<M, F, 4, false, true>), dim3(grid), dim3(kScanThreads), 0, s, in, xmul, out, \
-                       flags, n, desc, tiles, timeout, 1u)
+                       flags, n, desc, tiles, timeout, ep)
     if (flag_mode == 0) {
         if (xmul) SEG(0, true); else SEG(0, false);
     } else {

@@ -168,3 +168,44 @@ def test_spmv_scan_gpu_vs_fp64(gpu, shape, algo):
     b = sol.run().cpu().numpy()
     e = errors(reference_solution(prob), b)
     assert e["relL2"] < 1e-5, e
+
+
+@pytest.mark.gpu
+def test_lookback_epochs_reuse_workspace(gpu):
+    """Back-to-back look-back scans share one descriptor array with a new
+    epoch per launch (no memset): changing inputs, sizes, exclusive/inclusive,
+    dtypes and a segmented scan in between must all stay exact; then a
+    captured graph (epoch 0, memset inside the graph) replayed on new data,
+    followed by more eager scans."""
+    g = torch.Generator().manual_seed(7)
+    outs = []
+    for i in range(12):
+        n = [1 << 20, 3 << 18, 12345, 1 << 22][i % 4]
+        x = torch.randint(-50, 50, (n,), generator=g, dtype=torch.int32)
+        ex = bool(i % 3 == 1)
+        y = scan(x.to(gpu), exclusive=ex, algo="lookback")
+        ref = torch.cumsum(x.long(), 0)
+        if ex:
+            ref = ref - x.long()
+        outs.append((y, ref))
+        if i == 5:
+            f = torch.zeros(n, dtype=torch.uint8)
+            f[::1000] = 1
+            xs = torch.rand(n, generator=g)
+            segmented_scan(xs.to(gpu), f.to(gpu))
+    for y, ref in outs:
+        assert torch.equal(y.cpu().long(), ref)
+    x = torch.randint(-9, 9, (1 << 21,), dtype=torch.int32, device=gpu)
+    out = torch.empty_like(x)
+    scan(x, out=out, algo="lookback")  # warm-up outside the capture
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        scan(x, out=out, algo="lookback")
+    for _ in range(3):
+        x.copy_(torch.randint(-9, 9, (1 << 21,), dtype=torch.int32, generator=g).to(gpu))
+        graph.replay()
+        assert torch.equal(out.cpu().long(), torch.cumsum(x.cpu().long(), 0))
+        y = scan(x, algo="lookback")
+        assert torch.equal(y.cpu().long(), torch.cumsum(x.cpu().long(), 0))
+    assert not lookback_timed_out(gpu)
