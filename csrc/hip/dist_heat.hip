@@ -342,6 +342,29 @@ __global__ __launch_bounds__(64) void ipc_wait_kernel(FlagList l, unsigned value
     }
 }
 
+// Rehearsal only (transport 2 with CME_DIST_FAKE_XCHG_US > 0): stands in for
+// the network part of an exchange on the comm stream -- one wave that holds
+// the stream for a fixed wall-clock time, between the real pack and unpack
+// kernels -- so the border -> exchange -> border chain of an N-GPU run can be
+// timed on one GPU (benchmarks/bench_dist_rank.py --fake-xchg-us).
+__global__ __launch_bounds__(64) void delay_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int launch_delay_us(int us, hipStream_t s) {
+    static const long long khz = [] {
+        int dev = 0, rate = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate <= 0)
+            rate = 100000;  // 100 MHz
+        return (long long)rate;
+    }();
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, (unsigned long long)(khz * us / 1000));
+    CME_TRY(hipGetLastError());
+    return 0;
+}
+
 int launch_signal(const FlagList& l, unsigned v, hipStream_t s) {
     if (l.n == 0) return 0;
     hipLaunchKernelGGL(ipc_signal_kernel, dim3(1), dim3(64), 0, s, l, v);
@@ -733,7 +756,20 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         if (transport == 0)
             return post_exchange_rccl<T>(comm, subs[0], (T*)subs[0].buf[k], dt, ctx->sub[0].comm);
         if (transport == 3) return post_exchange_ipc<T>(subs[0], k, (unsigned)(++epoch), ctx->sub[0].comm);
-        if (transport == 2) return 0;
+        if (transport == 2) {
+            static const int fake_us = [] {
+                const char* e = getenv("CME_DIST_FAKE_XCHG_US");
+                return e ? atoi(e) : 0;
+            }();
+            if (fake_us <= 0) return 0;
+            for (int si = 0; si < nsub; ++si) {  // pack -> "network" -> unpack, as transport 0
+                SubCtx& u = ctx->sub[si];
+                CME_TRY_INT(pack_blocks<T>(subs[si], (T*)subs[si].buf[k], u.comm));
+                CME_TRY_INT(launch_delay_us(fake_us, u.comm));
+                CME_TRY_INT(unpack_blocks<T>(subs[si], (T*)subs[si].buf[k], u.comm));
+            }
+            return 0;
+        }
         for (int si = 0; si < nsub; ++si) {  // loopback: pack everything, then pull
             CME_TRY_INT(pack_blocks<T>(subs[si], (T*)subs[si].buf[k], ctx->sub[si].comm));
             CME_TRY(hipEventRecord(ctx->sub[si].ev_pack, ctx->sub[si].comm));

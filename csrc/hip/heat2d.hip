@@ -698,6 +698,11 @@ int streamn_chunk(int strips, int H, int chunk_hint, long cap) {
         const char* e = getenv("CME_STREAMN_THIN_WAVES");
         return e && atoi(e) > 0 ? (long)atoi(e) : 1024L;
     }();
+    static const int cap_pct = [] {  // share of the resident waves a bulk region may take
+        const char* e = getenv("CME_STREAMN_CAPPCT");
+        return e && atoi(e) > 0 ? atoi(e) : 100;
+    }();
+    cap = cap * cap_pct / 100;
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
         const long lo = 8 * RB > 32 ? 8 * RB : 32;
