@@ -193,6 +193,45 @@ __global__ __launch_bounds__(kThreads) void search_kernel(const T* __restrict__ 
     }
 }
 
+// Two-level search: every block first gathers S evenly spaced splitters
+// sorted[k*n/S] into LDS; a query binary-searches them there (log2 S LDS
+// reads instead of the top log2 S dependent global loads), then finishes in
+// the n/S-element bucket in global memory. Persistent grid: the splitter load
+// is amortised over many queries per block.
+template <typename T, bool UPPER, int S>
+__global__ __launch_bounds__(kThreads) void search2_kernel(const T* __restrict__ sorted, long long n,
+                                                           const T* __restrict__ q, long long m,
+                                                           long long* __restrict__ out) {
+    __shared__ T sp[S];
+    for (int k = threadIdx.x; k < S; k += kThreads) sp[k] = sorted[(long long)k * n / S];
+    __syncthreads();
+    for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < m; i += (long long)gridDim.x * kThreads) {
+        const T v = q[i];
+        // c = number of splitters strictly before the answer (a prefix: sp is sorted)
+        int c = 0;
+#pragma unroll
+        for (int half = S / 2; half > 0; half >>= 1) {
+            const T s = sp[c + half - 1];
+            if (UPPER ? !(v < s) : (s < v)) c += half;
+        }
+        if (c < S && (UPPER ? !(v < sp[c]) : (sp[c] < v))) ++c;  // S is a power of two: one more probe
+        long long lo = c == 0 ? 0 : (long long)(c - 1) * n / S + 1;
+        const long long hi = c == S ? n : (long long)c * n / S;
+        long long len = hi - lo;
+        while (len > 0) {
+            const long long half = len >> 1;
+            const T s = sorted[lo + half];
+            if (UPPER ? !(v < s) : (s < v)) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        out[i] = lo;
+    }
+}
+
 template <typename T, typename Op>
 __global__ __launch_bounds__(kThreads) void seg_reduce_kernel(const T* __restrict__ v,
                                                               const long long* __restrict__ offsets, long long nseg,
@@ -345,9 +384,23 @@ int select_impl(const U* x, const uint8_t* flags, long long n, int pred, U value
     CME_LAUNCH_STATUS();
 }
 
+// Splitter search when the sorted array is much longer than the splitter set
+// and there are enough queries per block to amortise loading it; the plain
+// one-level search otherwise (and for tiny inputs).
 template <typename T>
 int search_impl(const T* sorted, long long n, const T* q, long long m, int upper, long long* out, hipStream_t s) {
     if (m <= 0) return 0;
+    constexpr int S = sizeof(T) == 4 ? 4096 : 2048;
+    if (n >= 16LL * S && m >= 64LL * S) {
+        const long long blocks = (m + 16LL * kThreads - 1) / (16LL * kThreads);  // >= 16 queries per lane
+        const long long cap = 4LL * device_cu_count();
+        const dim3 grid((unsigned)(blocks < cap ? blocks : cap));
+        if (upper)
+            hipLaunchKernelGGL((search2_kernel<T, true, S>), grid, dim3(kThreads), 0, s, sorted, n, q, m, out);
+        else
+            hipLaunchKernelGGL((search2_kernel<T, false, S>), grid, dim3(kThreads), 0, s, sorted, n, q, m, out);
+        CME_LAUNCH_STATUS();
+    }
     const dim3 grid(stream_grid(m, kThreads));
     if (upper)
         hipLaunchKernelGGL((search_kernel<T, true>), grid, dim3(kThreads), 0, s, sorted, n, q, m, out);
@@ -464,4 +517,5 @@ CME_EXPORT int cme_inner_product(const void* a, const void* b, long long n, int 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(select_scatter_u32, 256, select_scatter_kernel<uint32_t, 0>);
 CME_REGISTER_KERNEL(search_i32, 256, search_kernel<int, false>);
+CME_REGISTER_KERNEL(search2_i32, 256, search2_kernel<int, false, 4096>);
 CME_REGISTER_KERNEL(arg_partial_f32, 256, arg_partial_kernel<float, true>);

@@ -56,9 +56,10 @@ def test_select_family_gpu(gpu, n, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32, torch.float64, torch.int64, torch.uint32])
 @pytest.mark.parametrize("upper", [False, True])
-def test_search_gpu(gpu, dtype, upper):
-    s = torch.sort(_data(200_001, torch.int64, hi=10_000)).values
-    q = _data(70_000, torch.int64, seed=5, lo=-5, hi=10_010)
+@pytest.mark.parametrize("m", [70_000, 300_000])  # 300K queries take the two-level splitter kernel
+def test_search_gpu(gpu, dtype, upper, m):
+    s = torch.sort(_data(200_001, torch.int64, hi=10_000)).values  # ~20 copies of each key: splitters inside runs
+    q = _data(m, torch.int64, seed=5, lo=-5, hi=10_010)
     if dtype == torch.uint32:
         q = q.clamp(min=0)
     s, q = s.to(dtype), q.to(dtype)
