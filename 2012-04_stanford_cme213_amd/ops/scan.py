@@ -84,10 +84,14 @@ def _run_ws(x: torch.Tensor) -> torch.Tensor:
     """Descriptors for launches that zero them natively and number their own
     epochs (spmv_scan_run, tuning arms): kept apart from :func:`_lookback_ws`,
     whose epoch count their words would otherwise collide with."""
-    tiles = (x.numel() + TILE - 1) // TILE
-    return workspace(x.device, 16 * tiles + 16 * (tiles // 64 + 1) + 64, f"lookback-run:{_ext.stream_ptr(x.device)}")
+    import ctypes
+
+    nbytes = ctypes.c_longlong(0)
+    _ext.call_hip("cme_spmv_scan_ws_bytes", x.numel(), ctypes.addressof(nbytes))
+    return workspace(x.device, nbytes.value, f"lookback-run:{_ext.stream_ptr(x.device)}")
 
 
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_ws_bytes", "qp")
 _ext.proto(_ext.HIP_PROTOS, "cme_lookback_timeout_word", "p")
 _timeout_word = None
 

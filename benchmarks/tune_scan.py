@@ -74,15 +74,18 @@ def spmv_main():
 
     _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_tune", "pppqipiip")
     s = _ext.stream_ptr()
-    for name in ("pwtk", "webbase-1M", "mac_econ_fwd500"):
+    mats = os.environ.get("CME_SPMV_MATS", "pwtk webbase-1M mac_econ_fwd500 jonheart").split()
+    modes = [int(m) for m in os.environ.get("CME_SPMV_MODES", "0 1 2 3 6 7").split()]
+    rows_list = [int(r) for r in os.environ.get("CME_SPMV_ROWS", "4 8 16").split()]
+    for name in mats:
         n, p, N = BENCH_SHAPES[name]
         sol = SpmvScanSolver(generate(n, p, 100000, N, seed=1), "cuda")
         ws = _run_ws(sol.a)
         a0 = sol.a.clone()
         ref = None
         from cme213x.ops.scan import _tw
-        for rows in (4, 8, 16):
-            for pf in (0, 1, 2, 3):  # bit 0 prefetch, bit 1 two-level look-back
+        for rows in rows_list:
+            for pf in modes:  # bit 0 prefetch, bit 1 two-level look-back, bit 2 one launch for all steps
                 f = lambda: _ext.call_hip("cme_spmv_scan_tune", sol.a.data_ptr(), sol.xx.data_ptr(),  # noqa
                                           sol.flags.data_ptr(), n, N, ws.data_ptr(), rows, pf, s)
                 sol.a.copy_(a0)

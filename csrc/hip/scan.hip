@@ -666,11 +666,22 @@ __device__ __forceinline__ SegRaw seg_load(const float* __restrict__ in, const f
 // before the look-back wait (two tiles of loads in flight per block).
 // Production: ROWS 4, no prefetch (benchmarks/tune_scan.py --spmv: prefetch
 // and 8 rows both lose to register pressure -- profiles/spmv_scan_tune.jsonl).
-template <int MODE, bool FUSED_MUL, int ROWS = 4, bool PREFETCH = false, bool LB2 = false>
+//
+// MULTI: `iters` in-place steps a <- segscan(a * xmul) in ONE launch (in ==
+// out). Block b owns tiles b, b+G, ... in every step and each lane re-reads
+// exactly the elements it wrote, so a step's input needs no cross-block
+// synchronisation -- only the look-back does. Step i has its OWN descriptor
+// set (`desc + i * desc_stride`, epoch `epoch + i`): blocks that own only
+// early tiles depend on nothing later and may run several steps ahead, so a
+// set may not be reused within a launch. Every wait depends only on earlier
+// (step, tile) pairs of a co-resident grid (processed in that order by every
+// block), so the smallest unfinished pair can always proceed.
+template <int MODE, bool FUSED_MUL, int ROWS = 4, bool PREFETCH = false, bool LB2 = false, bool MULTI = false>
 __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __restrict__ in, const float* __restrict__ xmul,
                                                                float* __restrict__ out, const void* __restrict__ flags,
-                                                               long long n, uint64_t* desc, int tiles,
-                                                               unsigned* timeout, uint32_t epoch) {
+                                                               long long n, uint64_t* desc0, int tiles,
+                                                               unsigned* timeout, uint32_t epoch0, int iters = 1,
+                                                               long long desc_stride = 0) {
     constexpr int TILE = kScanThreads * 4 * ROWS;
     constexpr int WAVE_ELEMS = kWave * 4 * ROWS;
     __shared__ float s_wv_[2][kScanWaves];
@@ -679,12 +690,19 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     int parity = 0;
+    // MULTI runs in place: every load goes through `out` (a restrict pointer
+    // must be the only path to the data it modifies)
+    const float* src = MULTI ? (const float*)out : in;
     SegRaw raw[ROWS];
     if (blockIdx.x < tiles) {
         const long long b0 = (long long)blockIdx.x * TILE + wid * WAVE_ELEMS;
 #pragma unroll
-        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, b0 + k * 256 + lane * 4, n);
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(src, xmul, flags, b0 + k * 256 + lane * 4, n);
     }
+    const int nit = MULTI ? iters : 1;
+    for (int it = 0; it < nit; ++it) {
+    uint64_t* desc = desc0 + (MULTI ? it * desc_stride : 0);
+    const uint32_t epoch = epoch0 + (uint32_t)it;
     // persistent, co-resident grid (see scan_lookback_kernel)
     for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x, parity ^= 1) {
     float* s_wv = s_wv_[parity];
@@ -773,7 +791,7 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     if (PREFETCH && next < tiles) {
         const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
 #pragma unroll
-        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, nb + k * 256 + lane * 4, n);
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(src, xmul, flags, nb + k * 256 + lane * 4, n);
     }
     if (LB2 && wid == 0) {
         const float pre = lb2_lookback<float, true>(lb2_views(desc, tiles), tile, tiles, tot_v, hf, timeout, epoch);
@@ -810,9 +828,16 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
     if (!PREFETCH && next < tiles) {
         const long long nb = (long long)next * TILE + wid * WAVE_ELEMS;
 #pragma unroll
-        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(in, xmul, flags, nb + k * 256 + lane * 4, n);
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(src, xmul, flags, nb + k * 256 + lane * 4, n);
+    } else if (MULTI && next >= tiles && it + 1 < nit) {
+        // the next step starts at this block's first tile, which this lane
+        // stored earlier (the tile just stored, if the block owns only one)
+        const long long nb = (long long)blockIdx.x * TILE + wid * WAVE_ELEMS;
+#pragma unroll
+        for (int k = 0; k < ROWS; ++k) raw[k] = seg_load<MODE, FUSED_MUL>(src, xmul, flags, nb + k * 256 + lane * 4, n);
     }
     }  // tile loop
+    }  // step loop
 }
 
 // epoch 0: zero the descriptors first (one memset); epoch e > 0: the caller
@@ -1059,26 +1084,44 @@ CME_EXPORT int cme_segscan(const float* in, const float* xmul, float* out, const
 // Final-project driver: `iters` fused steps a <- segscan(a * xx) (bitmask
 // heads) with ONE descriptor memset; iteration i uses look-back epoch i+1.
 namespace {
-template <int ROWS, bool PF, bool LB2 = false>
+// MULTI: up to kSpmvScanSteps steps per launch, one descriptor set per step
+// (cme_spmv_scan_ws_bytes sizes the workspace for that; see segscan_kernel).
+constexpr int kSpmvScanSteps = 64;
+template <int ROWS, bool PF, bool LB2 = false, bool MULTI = false>
 int spmv_scan_launch(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
                      hipStream_t s) {
     constexpr long long TILE = 1024LL * ROWS;
     const int tiles = (int)((n + TILE - 1) / TILE);
-    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF, LB2>, kScanThreads);
+    static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, ROWS, PF, LB2, MULTI>, kScanThreads);
     const int grid = tiles < device_cu_count() * bpc ? tiles : device_cu_count() * bpc;
     unsigned* timeout = lb_host_timeout();
     if (!timeout) return (int)hipErrorOutOfMemory;
+    if (iters >= (1 << 24)) return (int)hipErrorInvalidValue;  // epochs are 24-bit
     uint64_t* desc = lb_descriptors(ws);
-    CME_TRY(hipMemsetAsync(ws, 0, LB2 ? lb2_ws_bytes(tiles) : lb_ws_bytes(tiles), s));
-    for (int it = 0; it < iters; ++it)
-        hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF, LB2>), dim3(grid), dim3(kScanThreads), 0, s, a, xx, a,
-                           flags, n, desc, tiles, timeout, (uint32_t)(it + 1));
+    const size_t set_bytes = LB2 ? lb2_ws_bytes(tiles) : lb_ws_bytes(tiles);
+    if constexpr (MULTI) {
+        const long long stride = (long long)((set_bytes + 255) / 256 * 256 / sizeof(uint64_t));
+        for (int it0 = 0; it0 < iters; it0 += kSpmvScanSteps) {
+            const int k = iters - it0 < kSpmvScanSteps ? iters - it0 : kSpmvScanSteps;
+            CME_TRY(hipMemsetAsync(ws, 0, 16 + k * stride * sizeof(uint64_t), s));
+            hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF, LB2, true>), dim3(grid), dim3(kScanThreads), 0, s, a,
+                               xx, a, flags, n, desc, tiles, timeout, 1u, k, stride);
+            CME_TRY(hipGetLastError());
+        }
+    } else {
+        CME_TRY(hipMemsetAsync(ws, 0, set_bytes, s));
+        for (int it = 0; it < iters; ++it)
+            hipLaunchKernelGGL((segscan_kernel<1, true, ROWS, PF, LB2>), dim3(grid), dim3(kScanThreads), 0, s, a, xx,
+                               a, flags, n, desc, tiles, timeout, (uint32_t)(it + 1), 1, 0LL);
+    }
     CME_LAUNCH_STATUS();
 }
 }  // namespace
 
-// Two-level look-back, 4 rows per lane; the next tile is prefetched behind
-// the look-back only when a block owns several tiles (a multi-round grid).
+// Default: all steps in one persistent launch per 64 steps (segscan_kernel
+// MULTI). CME_SPMVSCAN_MULTI=0 restores one launch per step: two-level
+// look-back, 4 rows per lane, the next tile prefetched behind the look-back
+// only when a block owns several tiles (a multi-round grid).
 // benchmarks/tune_scan.py --spmv (profiles/spmvscan_tune_r2.log), GB/s at the
 // 12 B/element model: pwtk 4821 (prefetch) / 4521, webbase-1M 4451 (no
 // prefetch) / 4157, mac_econ 2273 / 2027; round 1's one-level arm: 3931 /
@@ -1087,25 +1130,56 @@ CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flag
                                  void* stream) {
     if (n <= 0 || iters <= 0) return 0;
     const long long tiles = (n + 4095) / 4096;
+    static const bool multi = [] {  // CME_SPMVSCAN_MULTI=0: one launch per step (the round-2 path)
+        const char* e = getenv("CME_SPMVSCAN_MULTI");
+        return !(e && atoi(e) == 0);
+    }();
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, 4, true, true>, kScanThreads);
-    if (tiles > 2LL * device_cu_count() * bpc)
-        return spmv_scan_launch<4, true, true>(a, xx, flags, n, iters, ws, as_stream(stream));
-    return spmv_scan_launch<4, false, true>(a, xx, flags, n, iters, ws, as_stream(stream));
+    hipStream_t s = as_stream(stream);
+    if (multi) {
+        // tile size and prefetch by the 4096-element tile count (tune_scan.py
+        // --spmv over the 15 benchmark shapes, profiles/spmvscan_multi_r2.log):
+        // short vectors want small tiles (more blocks on the look-back chain),
+        // long ones 16-B x 4 rows per lane and the next tile in flight
+        if (tiles <= 64) return spmv_scan_launch<1, false, true, true>(a, xx, flags, n, iters, ws, s);
+        if (tiles < 400) return spmv_scan_launch<2, false, true, true>(a, xx, flags, n, iters, ws, s);
+        return tiles >= 900 ? spmv_scan_launch<4, true, true, true>(a, xx, flags, n, iters, ws, s)
+                            : spmv_scan_launch<4, false, true, true>(a, xx, flags, n, iters, ws, s);
+    }
+    const bool pf = tiles > 2LL * device_cu_count() * bpc;
+    return pf ? spmv_scan_launch<4, true, true>(a, xx, flags, n, iters, ws, s)
+              : spmv_scan_launch<4, false, true>(a, xx, flags, n, iters, ws, s);
+}
+
+// Workspace bytes cme_spmv_scan_run / _tune need for n elements (one 256-B
+// aligned descriptor set of the finest tiling -- 1024 elements per tile -- per
+// step of a launch).
+CME_EXPORT int cme_spmv_scan_ws_bytes(long long n, long long* bytes) {
+    const long long tiles = (n + 1023) / 1024;
+    const long long set = (long long)(lb_ws_bytes(tiles) > lb2_ws_bytes(tiles) ? lb_ws_bytes(tiles) : lb2_ws_bytes(tiles));
+    *bytes = kSpmvScanSteps * ((set + 255) / 256 * 256) + 256;
+    return 0;
 }
 
 // Tuning entry (benchmarks/tune_scan.py --spmv): rows 4/8/16 x mode: bit 0
-// prefetch the next tile before the look-back, bit 1 two-level look-back.
+// prefetch the next tile before the look-back, bit 1 two-level look-back,
+// bit 2 all steps in one launch (with bit 1).
 CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* flags, long long n, int iters, void* ws,
                                   int rows, int mode, void* stream) {
     if (n <= 0 || iters <= 0) return 0;
     hipStream_t s = as_stream(stream);
-#define SPT(R)                                                                       \
-    switch (mode & 3) {                                                              \
-        case 0: return spmv_scan_launch<R, false, false>(a, xx, flags, n, iters, ws, s); \
-        case 1: return spmv_scan_launch<R, true, false>(a, xx, flags, n, iters, ws, s);  \
-        case 2: return spmv_scan_launch<R, false, true>(a, xx, flags, n, iters, ws, s);  \
-        default: return spmv_scan_launch<R, true, true>(a, xx, flags, n, iters, ws, s);  \
+#define SPT(R)                                                                             \
+    switch (mode & 7) {                                                                    \
+        case 0: return spmv_scan_launch<R, false, false>(a, xx, flags, n, iters, ws, s);       \
+        case 1: return spmv_scan_launch<R, true, false>(a, xx, flags, n, iters, ws, s);        \
+        case 2: return spmv_scan_launch<R, false, true>(a, xx, flags, n, iters, ws, s);        \
+        case 3: return spmv_scan_launch<R, true, true>(a, xx, flags, n, iters, ws, s);         \
+        case 6: return spmv_scan_launch<R, false, true, true>(a, xx, flags, n, iters, ws, s);  \
+        case 7: return spmv_scan_launch<R, true, true, true>(a, xx, flags, n, iters, ws, s);   \
+        default: return (int)hipErrorInvalidValue;                                         \
     }
+    if (rows == 1) SPT(1)
+    if (rows == 2) SPT(2)
     if (rows == 4) SPT(4)
     if (rows == 8) SPT(8)
     if (rows == 16) SPT(16)
