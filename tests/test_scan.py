@@ -171,6 +171,26 @@ def test_spmv_scan_gpu_vs_fp64(gpu, shape, algo):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1_200_000, 200_000, 70), (300_000, 20_000, 130)])
+def test_spmv_scan_fused_steps_long_runs(gpu, shape):
+    """The one-launch multi-step kernel on the 2-rows-per-lane tiling, with
+    more steps than one launch holds (64): the run is split into launches,
+    each with its own per-step descriptor sets."""
+    n, p, N = shape
+    prob = generate(n, p, 10000, N, seed=9)
+    sol = SpmvScanSolver(prob, gpu, "lookback")
+    b = sol.run().cpu().numpy()
+    step = SpmvScanSolver(prob, gpu, "lookback")  # one segmented_scan launch per step
+    for _ in range(N):
+        step.step()
+    e_steps = errors(step.a.cpu().numpy().astype(np.float64), b)
+    assert e_steps["relL2"] < 2e-6 * N, e_steps  # same arithmetic; tiling changes the association only
+    e = errors(reference_solution(prob), b)
+    assert e["relL2"] < 2e-6 * N, e  # fp32 rounding grows with the number of steps
+    assert not lookback_timed_out(gpu)
+
+
+@pytest.mark.gpu
 def test_lookback_epochs_reuse_workspace(gpu):
     """Back-to-back look-back scans share one descriptor array with a new
     epoch per launch (no memset): changing inputs, sizes, exclusive/inclusive,
