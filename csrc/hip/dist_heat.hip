@@ -804,9 +804,20 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         CME_TRY(hipStreamWaitEvent(u.border, u.ev_start, 0));
         CME_TRY(hipStreamWaitEvent(u.comm, u.ev_start, 0));
     }
+    // Events recorded by THIS call. Everything an earlier call queued is
+    // already ordered before ev_start (the caller's stream joined all of it),
+    // so waits on events of earlier calls are skipped: redundant in eager
+    // mode, and not allowed while the caller's stream is being captured into
+    // a hipGraph (a graph may only depend on work captured with it).
+    bool comm_rec = false, int_rec[2] = {false, false}, border_rec[2] = {false, false};
+    auto wait_if = [&](hipStream_t st, hipEvent_t ev, bool rec) -> int {
+        if (rec) CME_TRY(hipStreamWaitEvent(st, ev, 0));
+        return 0;
+    };
     if (exchange_first) {  // make the halos of the current state valid
         CME_TRY_INT(exchange_all(cur));
         for (int si = 0; si < nsub; ++si) CME_TRY(hipEventRecord(ctx->sub[si].ev_comm, ctx->sub[si].comm));
+        comm_rec = true;
         for (int si = 0; si < nsub; ++si)
             for (int j = 0; j < nsub; ++j) CME_TRY(hipStreamWaitEvent(ctx->sub[si].compute, ctx->sub[j].ev_comm, 0));
     }
@@ -821,6 +832,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         }
         CME_TRY_INT(exchange_all(k));
         for (int si = 0; si < nsub; ++si) CME_TRY(hipEventRecord(ctx->sub[si].ev_comm, ctx->sub[si].comm));
+        comm_rec = true;
         return 0;
     };
     int pass = 0;
@@ -836,6 +848,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
+            border_rec[par] = true;
             CME_TRY_INT(post_comm(par, cur ^ 1));
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
@@ -848,35 +861,39 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
             // the exchange of the new borders overlaps the interior
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.compute, u.ev_comm, 0));
+                CME_TRY_INT(wait_if(u.compute, u.ev_comm, comm_rec));
                 for (int j = 0; j < npeer[si]; ++j)
-                    CME_TRY(hipStreamWaitEvent(u.compute, ctx->sub[peers[si][j]].ev_comm, 0));
+                    CME_TRY_INT(wait_if(u.compute, ctx->sub[peers[si][j]].ev_comm, comm_rec));
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.compute));
             }
+            border_rec[par] = true;
             CME_TRY_INT(post_comm(par, cur ^ 1));
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
                 CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
             }
+            int_rec[par] = true;
         } else {
             for (int si = 0; si < nsub; ++si) {  // border strips of pass i
                 SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.border, u.ev_comm, 0));
+                CME_TRY_INT(wait_if(u.border, u.ev_comm, comm_rec));
                 for (int j = 0; j < npeer[si]; ++j)
-                    CME_TRY(hipStreamWaitEvent(u.border, ctx->sub[peers[si][j]].ev_comm, 0));
-                CME_TRY(hipStreamWaitEvent(u.border, u.ev_int[par ^ 1], 0));
+                    CME_TRY_INT(wait_if(u.border, ctx->sub[peers[si][j]].ev_comm, comm_rec));
+                CME_TRY_INT(wait_if(u.border, u.ev_int[par ^ 1], int_rec[par ^ 1]));
                 CME_TRY_INT(sweep(si, subs[si].border, subs[si].n_b, cur, ns, u.border));
                 CME_TRY(hipEventRecord(u.ev_border[par], u.border));
             }
+            border_rec[par] = true;
             CME_TRY_INT(post_comm(par, cur ^ 1));  // halo exchange of the new state
             for (int si = 0; si < nsub; ++si) {  // deep interior, overlapping both
                 SubCtx& u = ctx->sub[si];
-                CME_TRY(hipStreamWaitEvent(u.compute, u.ev_border[par ^ 1], 0));
+                CME_TRY_INT(wait_if(u.compute, u.ev_border[par ^ 1], border_rec[par ^ 1]));
                 CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
                 CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
             }
+            int_rec[par] = true;
         }
         cur ^= 1;
         it += ns;
@@ -888,6 +905,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         CME_TRY(hipEventRecord(u.ev_border[0], u.border));
         CME_TRY(hipStreamWaitEvent(s, u.ev_int[0], 0));
         CME_TRY(hipStreamWaitEvent(s, u.ev_border[0], 0));
+        if (!comm_rec) CME_TRY(hipEventRecord(u.ev_comm, u.comm));  // join the comm stream in any case
         CME_TRY(hipStreamWaitEvent(s, u.ev_comm, 0));
     }
     if (transport == 3) *subs[0].ipc->epoch = epoch;
