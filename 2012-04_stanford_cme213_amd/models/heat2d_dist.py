@@ -141,7 +141,7 @@ class DistHeat:
 
     def __init__(self, params: SimParams, comm: Comm | None = None, dtype=torch.float32, device="cpu",
                  local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream",
-                 tblock: int = 1, fma: bool = False):
+                 tblock: int = 1, fma: bool = False, kernel: str = "streamn"):
         self.p = params
         self.comm = comm or LoopbackComm()
         self.world = world or self.comm.size
@@ -152,7 +152,14 @@ class DistHeat:
             raise ValueError("tblock must be 1..4")
         if tblock > 3 and dtype == torch.float64 and torch.device(device).type == "cuda":
             raise ValueError("tblock 4 (4-step passes) is fp32 only on the GPU")
+        if kernel not in ("streamn", "pipe"):
+            raise ValueError("kernel must be 'streamn' or 'pipe'")
+        if kernel == "pipe" and dtype == torch.float64 and tblock > 2 and torch.device(device).type == "cuda":
+            raise ValueError("the pipelined pass is fp32 only")
         self.fma = bool(fma)
+        # 3-4 step passes: streamN (one wave holds every step) or the
+        # wave-pipelined kernel (csrc/hip/heat_pipe.hip); identical results
+        self.kernel = kernel
         self.variant = "fma" if self.fma else variant
         self.tblock = tblock
         self.device = torch.device(device)
@@ -165,6 +172,11 @@ class DistHeat:
         self.iteration = 0
         # make halos consistent with the neighbours' initial state
         self.exchange(self._cur()).wait()
+
+    def _flags(self) -> int:
+        """Kernel flags of the native loop (cme_heat_dist_run): bit 0 FMA,
+        bit 1 the pipelined NS-step kernel."""
+        return int(self.fma) | (2 if self.kernel == "pipe" else 0)
 
     def _cur(self) -> int:
         return next(iter(self.subs.values())).grid.cur
@@ -272,7 +284,7 @@ class DistHeat:
                 regs = list(regions_of(s, self.tblock * g.B))
                 if regs:
                     heat_stepn(g.buf[k], g.buf[1 - k], regs, _ext_region(s), g.order, g.xcfl, g.ycfl, ns,
-                               fma=self.fma)
+                               fma=self.fma, kernel=self.kernel)
 
         if sync:
             sweep(_interior_regions)
@@ -447,7 +459,7 @@ class DistHeat:
         plan["subs"][0].ipc = ctypes.addressof(self._ipc_plan(ipc)["plan"]) if transport == 3 else None
         _ext.call_hip("cme_heat_dist_run", transport, rccl.handle if rccl is not None else None,
                       ctypes.addressof(plan["subs"]), len(self.subs), 0 if g0.dtype == torch.float32 else 1,
-                      g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock, int(self.fma),
+                      g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock, self._flags(),
                       ctypes.addressof(cur_out), _ext.stream_ptr(g0.device))
         for s in self.subs.values():
             s.grid.cur = cur_out.value

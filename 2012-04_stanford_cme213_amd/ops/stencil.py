@@ -22,7 +22,9 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f32", "ppiipipiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiipipiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f32", "ppiipipiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f64", "ppiipipiiddiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f32", "ppiipipiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
@@ -33,15 +35,17 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f64", "ppiiiiiidd")
 
 VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
             "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,
-            "stream4_fma": 10}
+            "stream4_fma": 10, "pipe3": 11, "pipe3_fma": 12, "pipe4": 13, "pipe4_fma": 14}
 # variants that advance more than one timestep per launch (multi-step drivers
 # only); stream4 (4 steps per HBM pass) is fp32 only, stream3 takes fp32 and
-# fp64 (one row per register block for doubles)
-MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma"}
-FP32_ONLY = {"stream4", "stream4_fma"}
+# fp64 (one row per register block for doubles); pipeN = the wave-pipelined
+# N-step pass (csrc/hip/heat_pipe.hip), fp32
+MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma", "pipe3", "pipe3_fma",
+             "pipe4", "pipe4_fma"}
+FP32_ONLY = {"stream4", "stream4_fma", "pipe3", "pipe3_fma", "pipe4", "pipe4_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
-FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma"}
+FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -100,14 +104,19 @@ def heat_step2(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, i
 
 
 def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, int, int, int], order: int,
-               xcfl: float, ycfl: float, nsteps: int, chunk: int = 0, fma: bool = False) -> None:
+               xcfl: float, ycfl: float, nsteps: int, chunk: int = 0, fma: bool = False,
+               kernel: str = "streamn") -> None:
     """``nsteps`` (2-4) timesteps in one HBM pass (temporal blocking): the
     intermediate steps cover ``ext`` (the output regions grown by at most
     (nsteps-1)*B cells, e.g. into an nsteps*B-deep halo), the last one writes
     ``curr`` on every region of ``regions`` (one tuple or a list of <= 4, one
     launch). Cells of ``ext`` outside the grid's update set keep their value.
     Bitwise equal to ``nsteps`` single steps; 4 steps are fp32 only.
+    ``kernel="pipe"`` (fp32, 3 or 4 steps) runs the wave-pipelined pass
+    (csrc/hip/heat_pipe.hip) instead of streamN: same cells, same bits.
     On CPU it runs exactly those single steps through temporaries."""
+    if kernel not in ("streamn", "pipe"):
+        raise ValueError("kernel must be 'streamn' or 'pipe'")
     _check(prev, curr)
     if isinstance(regions[0], int):
         regions = [regions]
@@ -137,6 +146,10 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
     r = (ctypes.c_int * len(flat))(*flat)
     e = (ctypes.c_int * 4)(*map(int, ext))
     name = "cme_heat_stepn_f64" if f64 else "cme_heat_stepn_f32"
+    if kernel == "pipe" and nsteps >= 3:
+        if f64:
+            raise ValueError("the pipelined pass is fp32 only")
+        name = "cme_heat_pipe_f32"
     _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), len(regions),
                   ctypes.addressof(e), order, nsteps, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
 

@@ -10,8 +10,8 @@ EXACTLY K timed steps bracketed by barrier + synchronize, max over ranks; rank
 A "step" is one full timestep of the global grid: the FTCS sweep of every
 point plus the halo exchange between neighbouring ranks (1-D stripes, async
 mode: deep interior overlapped with the exchange, borders after it). With
-``--tblock n`` (default: 3, or 4 when a rank holds <= 1/8 of 16384^2 --
-``auto_tblock``) n timesteps are fused into one HBM pass (temporal blocking)
+``--tblock n`` (default ``auto_tblock``: 4 with the wave-pipelined pass) n
+timesteps are fused into one HBM pass (temporal blocking)
 and each exchange moves nB-deep halos; K timed steps are still exactly K
 timesteps (a K that is not a multiple of n ends with a shorter pass).
 
@@ -63,7 +63,8 @@ def native_selftest(comm, native, dev, args) -> bool:
 
     p = SimParams(nx=1024, ny=1024, iters=6, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
-    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma))
+    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma),
+                 kernel=args.kernel)
     b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1, fma=bool(args.fma))
     # non-uniform interior so a stale or misplaced halo changes the answer
     for sim in (a, b):
@@ -93,14 +94,17 @@ def native_selftest(comm, native, dev, args) -> bool:
     return bool(bad.item() == 0)
 
 
-def auto_tblock(points_per_rank: int) -> int:
-    """Timesteps per pass for a subdomain size. Every wave of the fused pass
-    re-computes 2(NS-1)B warm-up rows, a per-pass cost fixed by the resident
-    wave count, not by the subdomain; a small subdomain amortises it over
-    more steps. Measured one-rank schedules (benchmarks/bench_dist_rank.py,
-    profiles/dist_rank_r2.md): 3 steps win at 16384^2 / 1, 2, 4 ranks
-    (0.181 / 0.0996 / 0.0584 ms/step vs 0.193 / 0.104 / 0.0596), 4 steps at
-    8 ranks (0.0307 vs 0.0321-0.0336)."""
+def auto_tblock(points_per_rank: int, kernel: str = "pipe") -> int:
+    """Timesteps per pass for a subdomain size and pass kernel.
+
+    streamN (one wave holds every step): each wave re-computes 2(NS-1)B
+    warm-up rows, a per-pass cost fixed by the resident wave count; 3 steps
+    win at 16384^2 / 1, 2, 4 ranks, 4 steps at 8 ranks (profiles/
+    dist_rank_r2.md).
+    pipe (steps split across the waves of a workgroup, csrc/hip/heat_pipe.hip):
+    4 steps win at every rank count (profiles/heat_pipe_r2.md)."""
+    if kernel == "pipe":
+        return 4
     return 4 if points_per_rank <= 16384 * 16384 // 8 else 3
 
 
@@ -123,6 +127,9 @@ def main() -> int:
     ap.add_argument("--tblock", type=int, choices=[0, 1, 2, 3, 4], default=0,
                     help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos); "
                          "0 = by subdomain size (auto_tblock)")
+    ap.add_argument("--kernel", choices=["pipe", "streamn"], default="pipe",
+                    help="3-4 step pass kernel: pipe = timesteps split across the waves of a workgroup "
+                         "(csrc/hip/heat_pipe.hip); streamn = every step in one wave (heat2d.hip)")
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: run the K-step loop in C++ over a native communicator (auto: after a "
                          "bitwise self-test against the torch.distributed loop)")
@@ -163,7 +170,7 @@ def main() -> int:
             torch.cuda.synchronize(dev)
 
     if args.tblock == 0:
-        args.tblock = auto_tblock(args.n * args.n // max(1, comm.size))
+        args.tblock = auto_tblock(args.n * args.n // max(1, comm.size), args.kernel)
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
@@ -210,7 +217,7 @@ def main() -> int:
     use_native = native is not None and native_ok
 
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
-                   fma=bool(args.fma))
+                   fma=bool(args.fma), kernel=args.kernel)
     init_state = {(s.blk.x0, s.blk.y0): s.grid.buf.clone() for s in sim.subs.values()} if on_gpu else {}
 
     def run(k):
@@ -290,8 +297,10 @@ def main() -> int:
                 "global_batch": pts,
                 "seq_len": 1,
                 "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
-                "variant": (args.variant if args.tblock == 1 else f"stream{args.tblock} ({args.tblock} steps/pass)")
-                + (" fma" if args.fma else " exact"),
+                "variant": (args.variant if args.tblock == 1 else
+                            f"{'pipe' if args.kernel == 'pipe' and args.tblock >= 3 else 'stream'}{args.tblock} "
+                            f"({args.tblock} steps/pass)") + (" fma" if args.fma else " exact"),
+                "kernel": args.kernel,
                 "fma": bool(args.fma),
                 "tblock": args.tblock,
                 "device": args.device,

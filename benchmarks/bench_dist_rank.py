@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--tblock", type=int, default=3, help="timesteps per exchange / HBM pass (1-4)")
     ap.add_argument("--native", type=int, default=1, help="1: native loop (null transport); 0: Python loop")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--kernel", default="streamn", choices=["streamn", "pipe"],
+                    help="3-4 step pass kernel: streamN or the wave-pipelined pass")
     args = ap.parse_args()
     import torch
 
@@ -53,7 +55,8 @@ def main():
     for w in args.world:
         rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
         p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=False, flavor="hw5")
-        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=bool(args.fma))
+        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=bool(args.fma),
+                      kernel=args.kernel)
 
         def run(k):
             if args.native:
@@ -74,6 +77,7 @@ def main():
         ms = sorted(times)[len(times) // 2]
         base = base or ms * w
         print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
+                          "kernel": args.kernel,
                           "reps": args.reps,
                           "ms_per_step": round(ms, 4),
                           "compute_scaling_eff": round(base / (ms * w), 3)}), flush=True)

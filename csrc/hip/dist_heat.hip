@@ -45,6 +45,9 @@ extern "C" int cme_heat_step_f64(const double* prev, double* curr, int pitch, in
 extern "C" int cme_heat_stepn_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
                                   void* stream);
+extern "C" int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                 const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
+                                 void* stream);
 extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
@@ -387,15 +390,20 @@ int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T 
 template <>
 int step_region<float>(const float* p, float* c, int pitch, int gy, const int* r, int order, float xcfl, float ycfl,
                        int fma, hipStream_t s) {
-    return cme_heat_step_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
+    return cme_heat_step_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, (fma & 1) ? 6 : 2, xcfl, ycfl, 0,
+                             (void*)s);
 }
 template <>
 int step_region<double>(const double* p, double* c, int pitch, int gy, const int* r, int order, double xcfl,
                         double ycfl, int fma, hipStream_t s) {
-    return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, fma ? 6 : 2, xcfl, ycfl, 0, (void*)s);
+    return cme_heat_step_f64(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, (fma & 1) ? 6 : 2, xcfl, ycfl, 0,
+                             (void*)s);
 }
 
-// ns-step pass (ns = 2..4) over n (<= 4) regions in one launch
+// ns-step pass (ns = 2..4) over n (<= 4) regions in one launch. `fma` bit 0:
+// FMA-contracted stencil; bit 1 (kKernelPipe): 3-4 step fp32 passes run the
+// wave-pipelined kernel (heat_pipe.hip) instead of streamN -- same bits.
+constexpr int kKernelPipe = 2;
 template <typename T>
 int stepn_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, int ns,
                   T xcfl, T ycfl, int fma, hipStream_t s);
@@ -403,12 +411,14 @@ int stepn_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, cons
 template <>
 int stepn_regions<float>(const float* p, float* c, int pitch, int gy, const int* r, int n, const int* ext, int order,
                          int ns, float xcfl, float ycfl, int fma, hipStream_t s) {
-    return cme_heat_stepn_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma, (void*)s);
+    if ((fma & kKernelPipe) && ns >= 3)
+        return cme_heat_pipe_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
+    return cme_heat_stepn_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
 }
 template <>
 int stepn_regions<double>(const double* p, double* c, int pitch, int gy, const int* r, int n, const int* ext,
                           int order, int ns, double xcfl, double ycfl, int fma, hipStream_t s) {
-    return cme_heat_stepn_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma, (void*)s);
+    return cme_heat_stepn_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
 }
 
 // ------------------------------------------------------------- distributed loop
@@ -921,7 +931,8 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
 // process, neighbours' memory mapped through SubDesc.ipc). dtype 0 f32, 1 f64.
 // tblock n (1-4): n steps per exchange (nB-deep halos, `interior` shrunk by
 // nB on neighbour sides, `ext` = owned region grown by (n-1)B on neighbour
-// sides; 4 fp32 only). fma: FMA-contracted stencil.
+// sides; 4 fp32 only). fma bit 0: FMA-contracted stencil; bit 1: 3-4 step
+// fp32 passes on the wave-pipelined kernel (kKernelPipe).
 CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, int nsub, int dtype, int order,
                                  double xcfl, double ycfl, int iters, int cur, int sync, int exchange_first,
                                  int tblock, int fma, int* cur_out, void* stream) {

@@ -22,6 +22,7 @@
 //            next RB rows are prefetched while the current RB are computed.
 //            Each input element is fetched from HBM ~once: 8 B/pt fp32.
 #include "cme213/common.h"
+#include "cme213/heat_region.h"
 #include "cme213/heat_stencil.h"
 #include "cme213/vec.h"
 
@@ -201,7 +202,6 @@ __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restri
 //  * FMA=true evaluates the FMA-contracted stencil (heat_update_fma).
 constexpr int kStrip2Out = 60 * 4;
 
-constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 
 template <typename T, int ORDER, int RB, bool FMA, bool CHECK>
 struct Stream2 {
@@ -340,15 +340,6 @@ __device__ __forceinline__ void stream2_run(const T* src, T* dst, int pitch, int
     st.run();
 }
 
-// Up to four output regions per launch (a distributed subdomain's border
-// strips go out as ONE launch); every region shares the step-1 region.
-constexpr int kMaxS2Regions = 4;
-struct S2Regions {
-    int n;
-    int xb[kMaxS2Regions], xe[kMaxS2Regions], yb[kMaxS2Regions], ye[kMaxS2Regions];
-    int strips[kMaxS2Regions], chunk[kMaxS2Regions];
-    int wave_end[kMaxS2Regions];  // cumulative wave counts
-};
 
 template <typename T, int ORDER, int RB, bool FMA, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void heat_stream2_kernel(
@@ -401,10 +392,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // (NS-k)B) feed no stored value: their arithmetic is skipped (wave-uniform).
 // Intermediate cells outside the `ext` region keep their input value (fixed
 // boundary cells), so the result equals NS single steps bit for bit.
-template <int NS>
-struct StripN {
-    static constexpr int kOut = (64 - 2 * NS) * 4;
-};
 
 template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD = 1, bool NT = false>
 struct StreamN {
@@ -602,9 +589,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 // ---------------------------------------------------------------- launchers
-struct Region {
-    int xb, xe, yb, ye;
-};
 
 // Two-step pass: output region `g`; step-1 (intermediate) region `g1` must
 // contain g and may extend at most B cells beyond it (into a 2B-deep halo,
@@ -769,6 +753,15 @@ int launch_stream2(const T* prev, T* curr, int pitch, int gy, Region g, Region g
 namespace {
 
 
+}  // namespace
+
+// heat_pipe.hip: the wave-pipelined NS-step pass (variants 11-14, fp32)
+extern "C" int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                 const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
+                                 void* stream);
+
+namespace {
+
 template <typename T, int ORDER>
 int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, int chunk_hint,
                 hipStream_t s) {
@@ -810,6 +803,15 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
                 default: return launch_streamn_multi<T, ORDER, 4, true>(prev, curr, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                         chunk_hint, s);
             }
+        } else {
+            return (int)hipErrorInvalidValue;
+        }
+    } else if (variant >= 11 && variant <= 14) {
+        // wave-pipelined NS = 3 (11 exact, 12 FMA) / 4 (13, 14) steps per pass
+        if constexpr (sizeof(T) == 4) {
+            const int r[4] = {g.xb, g.xe, g.yb, g.ye};
+            return cme_heat_pipe_f32(prev, curr, pitch, gy, r, 1, r, ORDER, variant <= 12 ? 3 : 4, xcfl, ycfl,
+                                     chunk_hint, (variant & 1) ? 0 : 1, s);
         } else {
             return (int)hipErrorInvalidValue;
         }
@@ -978,7 +980,8 @@ CME_EXPORT int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, i
 
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO
 // steps), 5 stream2 FMA (TWO steps), 6 stream FMA, 7 / 8 stream3 exact / FMA
-// (THREE steps, fp32), 9 / 10 stream4 exact / FMA (FOUR steps, fp32)
+// (THREE steps, fp32), 9 / 10 stream4 exact / FMA (FOUR steps, fp32),
+// 11 / 12 pipe3 exact / FMA, 13 / 14 pipe4 exact / FMA (wave-pipelined, fp32)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -1003,9 +1006,9 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int cur = 0;
     T* bufs[2] = {a, b};
     int i = 0;
-    if (variant >= 7 && variant <= 10) {
+    if (variant >= 7 && variant <= 14) {
         if (sizeof(T) != 4 && variant > 8) return (int)hipErrorInvalidValue;
-        const int ns = variant <= 8 ? 3 : 4;
+        const int ns = (variant <= 8 || variant == 11 || variant == 12) ? 3 : 4;
         for (; i + ns <= iters; i += ns) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
             if (rc) return rc;

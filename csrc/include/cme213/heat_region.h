@@ -1,0 +1,32 @@
+// Compute-region descriptors shared by the multi-step heat kernels
+// (heat2d.hip: stream2 / streamN; heat_pipe.hip: the wave-pipelined pass).
+#pragma once
+
+namespace cme {
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+// A rectangle of cells [xb, xe) x [yb, ye) of a device grid.
+struct Region {
+    int xb, xe, yb, ye;
+};
+
+// Up to four output regions per launch (a distributed subdomain's border
+// strips go out as ONE launch); every region shares the intermediate-step
+// region passed next to it.
+constexpr int kMaxS2Regions = 4;
+struct S2Regions {
+    int n;
+    int xb[kMaxS2Regions], xe[kMaxS2Regions], yb[kMaxS2Regions], ye[kMaxS2Regions];
+    int strips[kMaxS2Regions], chunk[kMaxS2Regions];
+    int wave_end[kMaxS2Regions];  // cumulative wave (or workgroup-task) counts
+};
+
+// Output columns of one 64-lane strip of an NS-step pass (4 columns per lane;
+// step k is valid on lanes k..63-k, x-neighbours arrive through DPP).
+template <int NS>
+struct StripN {
+    static constexpr int kOut = (64 - 2 * NS) * 4;
+};
+
+}  // namespace cme

@@ -22,4 +22,5 @@ step stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sta
 step fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o heat -- python3 $B
 step write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o heat -- python3 $B
 step sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/sq" -o heat -- python3 $B
+step wait 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/wait" -o heat -- python3 $B
 echo all-ok

@@ -119,6 +119,43 @@ def test_native_loop_loopback_transport(gpu, method, world, sync, tblock, fma, d
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("method,world", [(1, 4), (2, 4), (2, 6), (1, 3)])
+@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("tblock,fma", [(3, False), (3, True), (4, False), (4, True)])
+@pytest.mark.parametrize("native", [True, False])
+def test_pipe_kernel_subdomains_gpu(gpu, method, world, sync, tblock, fma, native):
+    """The wave-pipelined 3-4 step pass (csrc/hip/heat_pipe.hip) on the
+    distributed schedule -- deep interior, border strips in one launch,
+    intermediate steps into the nB-deep halos -- through the native loop
+    (loopback transport) and the Python loop: equal to the single-grid CPU
+    oracle bit for bit."""
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    p = SimParams(nx=333, ny=270, order=8, iters=9, sync=sync, grid_method=method, ic=5.0,
+                  bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
+    ref = DistHeat(p, None, torch.float32, "cpu", variant="naive", fma=fma)
+    sim = DistHeat(p, None, torch.float32, gpu, local_ranks=list(range(world)), world=world, tblock=tblock, fma=fma,
+                   kernel="pipe")
+    for d in (ref, sim):
+        for s in d.subs.values():
+            g, b = s.grid, s.blk
+            H = g.H
+            yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
+            ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0).to(torch.float32)
+            g.buf[:, H:H + b.ny, H:H + b.nx] = ic.to(g.device)
+        d.exchange(d._cur()).wait()
+    ref.run(p.iters)
+    if native:
+        sim.run_native(5)
+        sim.run_native(4)
+    else:
+        sim.run(p.iters)
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tblock,fma", [(1, False), (2, True), (4, True)])
 def test_native_loop_checkpoint_restart_gpu(gpu, tmp_path, tblock, fma):
     """Native loop on GPU subdomains: run 3, checkpoint, run 4 more; a fresh

@@ -16,7 +16,8 @@ import torch
 
 from dist_util import run_ranks
 
-# (grid_method, sync, tblock, fma, dtype)
+# (grid_method, sync, tblock, fma, dtype[, kernel]); kernel "pipe" = the
+# wave-pipelined 3-4 step pass (csrc/hip/heat_pipe.hip), default streamN
 CASES_2 = [
     (1, False, 1, False, "float32"),
     (1, True, 2, True, "float64"),
@@ -24,6 +25,8 @@ CASES_2 = [
     (1, False, 4, False, "float32"),
     (2, False, 2, False, "float32"),
     (2, True, 3, True, "float32"),
+    (1, False, 4, True, "float32", "pipe"),
+    (2, True, 3, False, "float32", "pipe"),
 ]
 CASES_4 = [
     (2, False, 1, False, "float32"),
@@ -33,6 +36,8 @@ CASES_4 = [
     (1, False, 3, True, "float32"),
     (1, True, 1, False, "float64"),
     (2, False, 3, True, "float64"),
+    (1, False, 4, True, "float32", "pipe"),
+    (2, False, 4, False, "float32", "pipe"),
 ]
 
 
@@ -64,9 +69,10 @@ def _ipc_rank(rank, world, cases):
     torch.cuda.set_device(0)
     comm = TorchComm()
     out = []
-    for method, sync, tblock, fma, dt in cases:
+    for method, sync, tblock, fma, dt, *kern in cases:
         dtype = getattr(torch, dt)
-        sim = DistHeat(_params(method, sync), comm, dtype, "cuda:0", tblock=tblock, fma=fma)
+        sim = DistHeat(_params(method, sync), comm, dtype, "cuda:0", tblock=tblock, fma=fma,
+                       kernel=kern[0] if kern else "streamn")
         _set_ic(sim, dtype)
         ipc = NativeIpc()
         sim.run_native(3, ipc=ipc)
@@ -84,7 +90,7 @@ def _check(world, cases):
     from cme213x.models.heat2d_dist import DistHeat
 
     parts = run_ranks(_ipc_rank, world, (cases,), timeout=240)
-    for ci, (method, sync, tblock, fma, dt) in enumerate(cases):
+    for ci, (method, sync, tblock, fma, dt, *_) in enumerate(cases):
         dtype = getattr(torch, dt)
         p = _params(method, sync)
         ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)

@@ -1,0 +1,156 @@
+"""Wave-pipelined NS-step heat pass (csrc/hip/heat_pipe.hip): bitwise equal to
+NS single steps (exact and FMA oracles) and to the streamN pass, over full
+grids, sub-regions, several output regions with a grown intermediate region
+(the distributed border-strip pass), every tuning arm (rows per phase,
+prefetch depth, chunking) and 5-6 steps per pass.
+
+Parity: the reference's hw2/hw5 update loops (hw/hw2/solution/2dHeat_solution.cu
+:413-530, hw/hw5/2dHeat_solution.cpp:501-628) applied NS times."""
+import numpy as np
+import pytest
+import torch
+
+from cme213x.models.heat2d import HeatGrid
+from cme213x.utils.params import SimParams
+from cme213x.utils.ulp import ulp_distance
+
+
+def _rand_grid(p, dtype, device="cpu", seed=0):
+    g = HeatGrid(p, dtype, device)
+    gen = torch.Generator().manual_seed(seed)
+    r = torch.rand(g.buf[0].shape, generator=gen, dtype=dtype)
+    g.buf[0].copy_(r)
+    g.buf[1].copy_(r)
+    return g
+
+
+def test_pipe_variants_are_fp32_multistep():
+    from cme213x.ops.stencil import FMA_VARIANTS, FP32_ONLY, MULTISTEP, VARIANTS, heat_run
+    for v in ("pipe3", "pipe3_fma", "pipe4", "pipe4_fma"):
+        assert v in VARIANTS and v in MULTISTEP and v in FP32_ONLY
+    assert "pipe4_fma" in FMA_VARIANTS and "pipe4" not in FMA_VARIANTS
+    p = SimParams(nx=20, ny=20, order=8)
+    g = HeatGrid(p, torch.float64)
+    with pytest.raises(ValueError):
+        heat_run(g.buf[0], g.buf[1], g.interior, 8, g.xcfl, g.ycfl, 3, "pipe3")
+
+
+def test_pipe_kernel_name_checked():
+    from cme213x.ops.stencil import heat_stepn
+    p = SimParams(nx=20, ny=20, order=8)
+    g = HeatGrid(p, torch.float32)
+    with pytest.raises(ValueError):
+        heat_stepn(g.buf[0], g.buf[1], g.interior, g.interior, 8, g.xcfl, g.ycfl, 3, kernel="bogus")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("iters", [1, 4, 7, 9])
+def test_gpu_pipe_temporal_blocking_bitwise(gpu, order, ns, fma, iters):
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    c.run(iters, "fma" if fma else "naive")
+    g.run(iters, f"pipe{ns}" + ("_fma" if fma else ""))
+    torch.cuda.synchronize()
+    d = ulp_distance(c.state(), g.state())
+    assert int(d.max()) == 0, f"max ulp {int(d.max())}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("region", [(4, 300, 4, 100), (9, 250, 17, 77), (130, 131, 5, 200), (8, 292, 8, 242)])
+@pytest.mark.parametrize("chunk", [0, 8, 14, 400])
+@pytest.mark.parametrize("ns", [3, 4])
+def test_gpu_pipe_subregion(gpu, region, chunk, ns):
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    ca, cb = c.buf[0].clone(), c.buf[0].clone()
+    ga, gb = g.buf[0].clone(), g.buf[0].clone()
+    oc = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 2 * ns, "fma")
+    og = heat_run(ga, gb, region, 8, g.xcfl, g.ycfl, 2 * ns, f"pipe{ns}_fma", chunk)
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("fma", [False, True])
+def test_gpu_pipe_multi_region_ext(gpu, ns, fma):
+    """Several output regions in one launch with an intermediate region grown
+    past them (the distributed border-strip pass): equal to the CPU single
+    steps and to the streamN pass."""
+    from cme213x.ops.stencil import heat_stepn
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    regs = [(4, 304, 4, 40), (4, 304, 220, 254), (4, 40, 40, 220), (270, 304, 40, 220)]
+    ext = (4, 304, 4, 254)
+    oc, og, os_ = c.buf[0].clone(), g.buf[0].clone(), g.buf[0].clone()
+    heat_stepn(c.buf[0], oc, regs, ext, 8, c.xcfl, c.ycfl, ns, fma=fma)
+    heat_stepn(g.buf[0], og, regs, ext, 8, g.xcfl, g.ycfl, ns, fma=fma, kernel="pipe")
+    heat_stepn(g.buf[0], os_, regs, ext, 8, g.xcfl, g.ycfl, ns, fma=fma, kernel="streamn")
+    torch.cuda.synchronize()
+    assert torch.equal(oc, og.cpu())
+    assert torch.equal(og, os_)
+
+
+@pytest.mark.gpu
+def test_gpu_pipe_tuning_arms_bitwise(gpu):
+    """Every compiled tuning arm (ns 3-6, rows per phase, prefetch depth,
+    tasks per CU / explicit chunk) equals ns single FMA steps on an odd-sized
+    region of random data."""
+    from cme213x import _ext
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=1500, ny=700, order=8)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    region = (9, 1400, 6, 690)
+    xb, xe, yb, ye = region
+    oracle = {}
+    for ns in (3, 4, 5, 6):
+        ca, cb = c.buf[0].clone(), c.buf[0].clone()
+        oracle[ns] = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, ns, "fma").clone()
+    s = _ext.stream_ptr(g.buf[0].device)
+    arms = [(ns, rb, pd, pc, ch) for ns in (3, 4) for rb in (2, 4, 8) for pd in (1, 2) for pc, ch in ((2, 0), (0, 24))]
+    arms += [(ns, 4, pd, 3, 0) for ns in (5, 6) for pd in (1, 2)]
+    for ns, rb, pd, pc, ch in arms:
+        out = g.buf[0].clone()
+        _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, xb, xe, yb, ye,
+                      g.xcfl, g.ycfl, ch, rb, ns, pd, pc, s)
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), oracle[ns]), (ns, rb, pd, pc, ch)
+
+
+@pytest.mark.gpu
+def test_gpu_pipe_long_run_matches_streamn(gpu):
+    """A 16384-wide, 2048-row strip (one rank's share of an 8-GPU run) over 24
+    steps: pipelined and streamN passes agree bit for bit."""
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=4096, ny=1024, order=8)
+    g = _rand_grid(p, torch.float32, gpu, seed=3)
+    a1, b1 = g.buf[0].clone(), g.buf[0].clone()
+    a2, b2 = g.buf[0].clone(), g.buf[0].clone()
+    o1 = heat_run(a1, b1, g.interior, 8, g.xcfl, g.ycfl, 24, "pipe4_fma")
+    o2 = heat_run(a2, b2, g.interior, 8, g.xcfl, g.ycfl, 24, "stream4_fma")
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert np.isfinite(o1.cpu().numpy()).all()
+
+
+def test_dist_heat_kernel_option_cpu():
+    """DistHeat validates the pass kernel and, on CPU tensors, runs the
+    single-step oracle composition whatever the kernel."""
+    from cme213x.models.heat2d_dist import DistHeat
+    p = SimParams(nx=80, ny=90, order=8, iters=4, flavor="hw5")
+    with pytest.raises(ValueError):
+        DistHeat(p, None, torch.float32, "cpu", tblock=4, kernel="bogus")
+    a = DistHeat(p, None, torch.float32, "cpu", local_ranks=[0, 1], world=2, tblock=4, kernel="pipe")
+    b = DistHeat(p, None, torch.float32, "cpu", local_ranks=[0, 1], world=2, tblock=1)
+    assert a._flags() == 2 and b._flags() == 0
+    a.run(5)
+    b.run(5)
+    assert np.array_equal(a.gather_global(), b.gather_global())
