@@ -9,6 +9,10 @@ ms per TIMESTEP.
 
     TUNE_H=16384,2048 TUNE_NS=3,4 TUNE_RB=2,4,8 TUNE_PD=1,2 TUNE_PERCU=1,2,4,8 \\
         python benchmarks/tune_heat_pipe.py
+
+TUNE_PD codes: 1 / 2 input prefetch depth; 11 depth 1 + non-temporal stores;
+21 / 41 the same with two / four waves per timestep role (RB 4). TUNE_SPIN
+seconds of clock ramp first, TUNE_REPS launches per sample.
 """
 import json
 import os
@@ -84,6 +88,14 @@ def main():
             print(json.dumps({"MISMATCH": c, "n_bad": int(d.shape[0]), "first": d[:4].tolist()}), flush=True)
 
     out = g.buf[1]
+    # clock ramp: TUNE_SPIN seconds of back-to-back passes before timing
+    import time
+    t_end = time.perf_counter() + float(os.environ.get("TUNE_SPIN", "1.5"))
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            pipe(cfgs[0], hs[0], out)
+        torch.cuda.synchronize()
+    reps = int(os.environ.get("TUNE_REPS", "4"))
     for H in hs:
         arms = [("streamn", ns) for ns in nss if ns in (3, 4)] + [("pipe", c) for c in cfgs]
         times = {a: [] for a in arms}
@@ -93,11 +105,11 @@ def main():
                 f()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(4):
+                for _ in range(reps):
                     f()
                 e1.record()
                 e1.synchronize()
-                times[a].append(e0.elapsed_time(e1) / 4)
+                times[a].append(e0.elapsed_time(e1) / reps)
         for a in sorted(arms, key=lambda a: sorted(times[a])[2] / (a[1] if a[0] == "streamn" else a[1][0])):
             ns = a[1] if a[0] == "streamn" else a[1][0]
             ms = sorted(times[a])[2] / ns

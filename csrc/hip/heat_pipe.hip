@@ -33,20 +33,34 @@ using namespace cme;
 // than a streamN wave's, so the warm-up share per pass drops NS-fold. The
 // arithmetic per cell, the region masks and hence the result are those of
 // StreamN / NS single steps, bit for bit.
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT>
+//
+// WPR > 1 (waves per role): a role is WPR waves side by side, so a strip is
+// 64*WPR lanes wide and the 2*NS lanes each strip loses to the shrinking
+// valid range are amortised over WPR times more output columns (12.5 % of the
+// lanes at NS = 4, WPR = 1; 6.25 % at WPR = 2). The x-neighbours across the
+// seam between two waves of a role come from the LDS edge buffer: every wave
+// publishes the edge lanes (0 and 63) of the rows it receives in phase q; they
+// are the centre rows of phase q+1 (needs RB == B), which the neighbour wave
+// reads back as the `old` operand of its DPP shifts (the lane with no DPP
+// source keeps it). Three edge buffers, one barrier per phase.
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT, int WPR = 1>
 struct PipeN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
     static constexpr int P = NW / cgcd(NW, RB);
     static constexpr int Q = P * PD / cgcd(P, PD);
-    using Ring = V4<T>[2][RB][64];
+    static constexpr int LW = 64 * WPR;  // lanes per role (strip width / 4)
+    static_assert(WPR == 1 || (RB == B && sizeof(T) == 4), "pipe: WPR > 1 needs RB == B (order 8, RB 4), fp32");
+    using Ring = V4<T>[2][RB][LW];
+    using Edge = V4<T>[3][RB][WPR][2];
 
     V4<T> w[NW];        // window of step-k rows (k = this wave's role); slot j = row r0 - (k+1)B + j
     V4<T> nxt[PD][RB];  // role 0: input rows of the next PD phases, in flight
     Ring* ring;         // ring[k]: step-(k+1) rows from role k to role k+1
+    Edge* edge;         // edge[k]: seam lanes of the step-k rows role k received (WPR > 1)
     const T* src;
     T* dst;
-    int pitch, gy, xbase, lane;
+    int pitch, gy, xbase, lane, sub, glane, e3;
     bool out_lane, full_vec;
     int y0, y1, xb, xe, xb1, xe1, yb1, ye1;
     T xcfl, ycfl;
@@ -58,10 +72,19 @@ struct PipeN {
     }
 
     template <bool MASK>
-    __device__ __forceinline__ V4<T> upd(int s_lo, int row) const {
+    __device__ __forceinline__ V4<T> upd(int s_lo, int row, const V4<T>& ev) const {
         const V4<T> c = w[(s_lo + B) % NW];
-        const V4<T> L = wave_shr1(c);
-        const V4<T> R = wave_shl1(c);
+        V4<T> L, R;
+        if constexpr (WPR == 1) {
+            L = wave_shr1(c);
+            R = wave_shl1(c);
+        } else {  // lane 0 / 63 keep the neighbour wave's seam value
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                L[j] = dpp_move<kDppWaveShr1>(ev[j], c[j]);
+                R[j] = dpp_move<kDppWaveShl1>(ev[j], c[j]);
+            }
+        }
         T rowv[12];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -115,22 +138,35 @@ struct PipeN {
             constexpr int F = PH % PD;
 #pragma unroll
             for (int i = 0; i < RB; ++i) w[(S + 2 * B + i) % NW] = nxt[F][i];
-            if (r0 + PD * RB < y1 + (NS - 1) * B) {
+            // unconditional (row_ptr clamps to the grid): a guarded prefetch
+            // becomes a phi whose register copies wait on the loads just issued
 #pragma unroll
-                for (int i = 0; i < RB; ++i) nxt[F][i] = load4(row_ptr(r0 + PD * RB + B + i));
-            }
+            for (int i = 0; i < RB; ++i) nxt[F][i] = load4(row_ptr(r0 + PD * RB + B + i));
         } else {
 #pragma unroll
-            for (int i = 0; i < RB; ++i) w[(S + 2 * B + i) % NW] = ring[K - 1][par][i][lane];
+            for (int i = 0; i < RB; ++i) w[(S + 2 * B + i) % NW] = ring[K - 1][par][i][glane];
+        }
+        V4<T> ev[RB];
+        if constexpr (WPR > 1) {
+            // seam values of this phase's centre rows (received last phase),
+            // then publish the seam lanes of the rows just received
+            const int ns = lane == 0 ? (sub > 0 ? sub - 1 : 0) : (sub + 1 < WPR ? sub + 1 : sub);
+            const int pe = e3 == 0 ? 2 : e3 - 1;
+#pragma unroll
+            for (int i = 0; i < RB; ++i) ev[i] = edge[K][pe][i][ns][lane == 0 ? 1 : 0];
+            if (lane == 0 || lane == 63) {
+#pragma unroll
+                for (int i = 0; i < RB; ++i) edge[K][e3][i][sub][lane == 63 ? 1 : 0] = w[(S + 2 * B + i) % NW];
+            }
         }
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
             const int row = r0 - (ST - 1) * B + i;
             if constexpr (ST < NS) {
                 if (row >= y0 - (NS - ST) * B && row < y1 + (NS - ST) * B)
-                    ring[K][par][i][lane] = upd<CHECK>((S + i) % NW, row);
+                    ring[K][par][i][glane] = upd<CHECK>((S + i) % NW, row, ev[i]);
             } else if (row >= y0 && row < y1) {
-                const V4<T> o = upd<false>((S + i) % NW, row);
+                const V4<T> o = upd<false>((S + i) % NW, row, ev[i]);
                 T* d = dst + (size_t)row * pitch;
                 if constexpr (!CHECK) {
                     if (out_lane) store_out(d, o);
@@ -147,6 +183,7 @@ struct PipeN {
         }
         r0 += RB;
         ++q;
+        if constexpr (WPR > 1) e3 = e3 == 2 ? 0 : e3 + 1;
         __syncthreads();
         if constexpr (PH + 1 < Q)
             return phase<K, PH + 1>();
@@ -160,6 +197,7 @@ struct PipeN {
     __device__ __forceinline__ void run() {
         r0 = y0 - (NS - 1) * B;
         q = 0;
+        e3 = 0;
         if constexpr (K == 0) {
 #pragma unroll
             for (int i = 0; i < 2 * B; ++i) w[i] = load4(row_ptr(r0 - B + i));
@@ -167,7 +205,14 @@ struct PipeN {
             for (int f = 0; f < PD; ++f)
 #pragma unroll
                 for (int i = 0; i < RB; ++i) nxt[f][i] = load4(row_ptr(r0 + f * RB + B + i));
+            if constexpr (WPR > 1) {  // seams of the first phase's centre rows (window slots B..2B-1)
+                if (lane == 0 || lane == 63) {
+#pragma unroll
+                    for (int i = 0; i < RB; ++i) edge[0][2][i][sub][lane == 63 ? 1 : 0] = w[B + i];
+                }
+            }
         }
+        if constexpr (WPR > 1) __syncthreads();
 #pragma unroll
         for (int i = 0; i < K; ++i) __syncthreads();
         while (phase<K, 0>()) {
@@ -187,12 +232,16 @@ struct PipeN {
     }
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT>
-__device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64], int k, const T* src, T* dst, int pitch, int gy,
-                                          int xbase, int lane, bool out_lane, bool full_vec, int y0, int y1, int xb,
-                                          int xe, int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl) {
-    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT> st;
+template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT, int WPR>
+__device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64 * WPR], V4<T> (*edge)[3][RB][WPR][2], int k,
+                                          int sub, const T* src, T* dst, int pitch, int gy, int xbase, int lane,
+                                          bool out_lane, bool full_vec, int y0, int y1, int xb, int xe, int xb1,
+                                          int xe1, int yb1, int ye1, T xcfl, T ycfl) {
+    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR> st;
     st.ring = ring;
+    st.edge = edge;
+    st.sub = sub;
+    st.glane = sub * 64 + lane;
     st.src = src;
     st.dst = dst;
     st.pitch = pitch;
@@ -214,17 +263,20 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64], int k, const
     st.run_role(k);
 }
 
-// one workgroup (NS waves) per strip-chunk task; regions as for streamN
-template <typename T, int ORDER, int RB, int NS, bool FMA, int PD = 1, bool NT = false>
-__global__ __launch_bounds__(NS * 64) void heat_pipe_kernel(const T* __restrict__ prev, T* __restrict__ curr,
-                                                            int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
-                                                            int ye1, T xcfl, T ycfl) {
+// one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for streamN
+template <typename T, int ORDER, int RB, int NS, bool FMA, int PD = 1, bool NT = false, int WPR = 1>
+__global__ __launch_bounds__(NS * WPR * 64) void heat_pipe_kernel(const T* __restrict__ prev, T* __restrict__ curr,
+                                                                  int pitch, int gy, S2Regions R, int xb1, int xe1,
+                                                                  int yb1, int ye1, T xcfl, T ycfl) {
     static_assert(NS >= 2 && NS <= 6, "pipe: 2..6 steps per pass");
-    __shared__ V4<T> ring[NS - 1][2][RB][64];
+    __shared__ V4<T> ring[NS - 1][2][RB][64 * WPR];
+    __shared__ V4<T> edge[WPR > 1 ? NS : 1][3][RB][WPR][2];
     constexpr int B = HeatOrder<ORDER>::B;
-    constexpr int OUT = StripN<NS>::kOut;
+    constexpr int OUT = PipeOut<NS, WPR>::kOut;
+    constexpr int LW = 64 * WPR;
     const int lane = lane_id();
-    const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+    const int k = wv / WPR, sub = wv % WPR;
     int task = (int)blockIdx.x;
     if (task >= R.wave_end[R.n - 1]) return;  // whole workgroup
     int r = 0;
@@ -237,20 +289,22 @@ __global__ __launch_bounds__(NS * 64) void heat_pipe_kernel(const T* __restrict_
     const int y0 = yb + ck * chunk;
     const int y1 = min(ye, y0 + chunk);
     const int xs = (xb & ~3) + strip * OUT;
-    const int xbase = xs - 4 * NS + 4 * lane;
+    const int gl = sub * 64 + lane;
+    const int xbase = xs - 4 * NS + 4 * gl;
     const int xl = min(max(xbase, 0), pitch - 4);
-    const bool out_lane = (lane >= NS) && (lane <= 63 - NS) && (xbase < xe) && (xbase + 4 > xb);
+    const bool out_lane = (gl >= NS) && (gl <= LW - 1 - NS) && (xbase < xe) && (xbase + 4 > xb);
     const bool full_vec = (xbase >= xb) && (xbase + 4 <= xe);
     constexpr int reach = 4 * (NS - 1);
     const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
                         (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
     if (inside)
-        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT>(ring, k, prev + xl, curr + xl, pitch, gy, xbase, lane,
-                                                        out_lane, full_vec, y0, y1, xb, xe, xb1, xe1, yb1, ye1, xcfl,
-                                                        ycfl);
+        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR>(ring, edge, k, sub, prev + xl, curr + xl, pitch, gy,
+                                                             xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
+                                                             xe1, yb1, ye1, xcfl, ycfl);
     else
-        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT>(ring, k, prev + xl, curr + xl, pitch, gy, xbase, lane, out_lane,
-                                                       full_vec, y0, y1, xb, xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR>(ring, edge, k, sub, prev + xl, curr + xl, pitch, gy,
+                                                            xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
+                                                            xe1, yb1, ye1, xcfl, ycfl);
 }
 
 // Chunk rule for the pipelined pass, in workgroup tasks: a whole number of
@@ -297,15 +351,15 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
     return ((chunk + RB - 1) / RB) * RB;
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int RB, int PD = 1, bool NT = false>
+template <typename T, int ORDER, int NS, bool FMA, int RB, int PD = 1, bool NT = false, int WPR = 1>
 int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl, T ycfl,
                       int chunk_hint, int per_cu, hipStream_t s) {
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
     static const long resident = [] {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT>,
-                                                         NS * 64, 0) != hipSuccess || per_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR>,
+                                                         NS * WPR * 64, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         return (long)per_cu * device_cu_count();
     }();
@@ -315,7 +369,7 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         const Region& g = gs[i];
         const int H = g.ye - g.yb;
         if (H <= 0 || g.xe <= g.xb) continue;
-        const int strips = (int)cdiv(g.xe - (g.xb & ~3), StripN<NS>::kOut);
+        const int strips = (int)cdiv(g.xe - (g.xb & ~3), PipeOut<NS, WPR>::kOut);
         const int chunk = pipe_chunk<NS, RB>(strips, H, chunk_hint, per_cu, resident);
         const int k = R.n++;
         R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
@@ -325,8 +379,8 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         R.wave_end[k] = tasks;
     }
     if (R.n == 0) return 0;
-    hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT>), dim3(tasks), dim3(NS * 64), 0, s, prev, curr,
-                       pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
+    hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR>), dim3(tasks), dim3(NS * WPR * 64), 0, s,
+                       prev, curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
     CME_LAUNCH_STATUS();
 }
 
@@ -383,6 +437,16 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
             if constexpr (RB == 4)
                 return launch_pipe_multi<float, 8, NS, true, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
                                                                          per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 21:  // + two waves per role (seams through LDS)
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 41:  // + four waves per role
+            if constexpr (RB == 4 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
         default: return (int)hipErrorInvalidValue;
     }

@@ -29,4 +29,11 @@ struct StripN {
     static constexpr int kOut = (64 - 2 * NS) * 4;
 };
 
+// Output columns of one strip of the wave-pipelined pass: WPR waves side by
+// side per timestep role (64*WPR lanes, 4 columns each, NS lanes lost per side).
+template <int NS, int WPR>
+struct PipeOut {
+    static constexpr int kOut = (64 * WPR - 2 * NS) * 4;
+};
+
 }  // namespace cme

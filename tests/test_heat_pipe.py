@@ -126,6 +126,34 @@ def test_gpu_pipe_tuning_arms_bitwise(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("region", [(9, 1400, 6, 690), (130, 131, 5, 200), (4, 484, 4, 100), (600, 1100, 33, 47)])
+def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
+    """Two and four waves per timestep role (seam x-neighbours through the LDS
+    edge buffer): equal to ns single FMA steps on regions narrower than, equal
+    to and wider than one strip, with explicit short chunks and the default
+    chunk rule."""
+    from cme213x import _ext
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=1500, ny=700, order=8)
+    c = _rand_grid(p, torch.float32, seed=5)
+    g = _rand_grid(p, torch.float32, gpu, seed=5)
+    xb, xe, yb, ye = region
+    oracle = {}
+    for ns in (3, 4, 5, 6):
+        ca, cb = c.buf[0].clone(), c.buf[0].clone()
+        oracle[ns] = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, ns, "fma").clone()
+    s = _ext.stream_ptr(g.buf[0].device)
+    arms = [(ns, 21, pc, ch) for ns in (3, 4, 5, 6) for pc, ch in ((2, 0), (0, 12), (0, 0))]
+    arms += [(ns, 41, pc, ch) for ns in (3, 4) for pc, ch in ((1, 0), (0, 8), (0, 0))]
+    for ns, pd, pc, ch in arms:
+        out = g.buf[0].clone()
+        _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, xb, xe, yb, ye,
+                      g.xcfl, g.ycfl, ch, 4, ns, pd, pc, s)
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), oracle[ns]), (ns, pd, pc, ch)
+
+
+@pytest.mark.gpu
 def test_gpu_pipe_long_run_matches_streamn(gpu):
     """A 16384-wide, 2048-row strip (one rank's share of an 8-GPU run) over 24
     steps: pipelined and streamN passes agree bit for bit."""
