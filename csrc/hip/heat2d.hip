@@ -130,10 +130,10 @@ __global__ __launch_bounds__(WPB * 64) void heat_stream_kernel(const T* __restri
     for (int y = y0; y < y1; y += RB) {
 #pragma unroll
         for (int i = 0; i < RB; ++i) win[2 * B + i] = nxt[i];
-        if (y + RB < y1) {
+        // unconditional prefetch (row_ptr clamps): a guarded one compiles to a
+        // phi whose register copies wait on the loads just issued
 #pragma unroll
-            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(y + RB + B + i));
-        }
+        for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(y + RB + B + i));
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const V4<T> c = win[r + B];
@@ -269,10 +269,8 @@ struct Stream2 {
         constexpr int S = (PH * RB) % NW;  // ring slot of logical row 0
 #pragma unroll
         for (int i = 0; i < RB; ++i) in[(S + 2 * B + i) % NW] = nxt[i];
-        if (r0 + RB - B < y1) {
 #pragma unroll
-            for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));
-        }
+        for (int i = 0; i < RB; ++i) nxt[i] = load4(row_ptr(r0 + RB + B + i));  // unguarded, as above
 #pragma unroll
         for (int i = 0; i < RB; ++i) s1[(S + 2 * B + i) % NW] = upd<CHECK>(in, (S + i) % NW, r0 + i);
 #pragma unroll
@@ -472,10 +470,8 @@ struct StreamN {
         constexpr int F = PH % PD;
 #pragma unroll
         for (int i = 0; i < RB; ++i) w[0][(S + 2 * B + i) % NW] = nxt[F][i];
-        if (r0 + PD * RB < y1 + (NS - 1) * B) {
 #pragma unroll
-            for (int i = 0; i < RB; ++i) nxt[F][i] = load4(row_ptr(r0 + PD * RB + B + i));
-        }
+        for (int i = 0; i < RB; ++i) nxt[F][i] = load4(row_ptr(r0 + PD * RB + B + i));  // unguarded, as above
         inter<1, S>();
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
