@@ -32,6 +32,8 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f64", "ppiiiiiiddi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fma_f64", "ppiiiiiidd")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fast_f32", "ppiiiiiiff")
+_ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fast_f64", "ppiiiiiidd")
 
 VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
             "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,

@@ -13,9 +13,11 @@ using namespace cme;
 
 namespace {
 
-template <typename T, int ORDER, bool FMA>
+// FMA: 0 exact (contraction off), 1 FMA-contracted, 2 reassociated ("fast")
+template <typename T, int ORDER, int FMA>
 void heat_region(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int ye, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
+    const HeatFast<ORDER, T> fc = heat_fast_coefs<ORDER>(xcfl, ycfl);
 #pragma omp parallel for schedule(static)
     for (int y = yb; y < ye; ++y) {
         const T* row = prev + (size_t)y * pitch;
@@ -28,12 +30,15 @@ void heat_region(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int 
                 ym[k] = row[x - (ptrdiff_t)(k + 1) * pitch];
                 yp[k] = row[x + (ptrdiff_t)(k + 1) * pitch];
             }
-            out[x] = heat_update_sel<ORDER, FMA>(row[x], xm, xp, ym, yp, xcfl, ycfl);
+            if constexpr (FMA == 2)
+                out[x] = heat_update_fast<ORDER>(row[x], xm, xp, ym, yp, fc);
+            else
+                out[x] = heat_update_sel<ORDER, FMA == 1>(row[x], xm, xp, ym, yp, xcfl, ycfl);
         }
     }
 }
 
-template <typename T, bool FMA = false>
+template <typename T, int FMA = 0>
 int heat_dispatch(const T* prev, T* curr, int pitch, int xb, int xe, int yb, int ye, int order, T xcfl, T ycfl) {
     switch (order) {
         case 2: heat_region<T, 2, FMA>(prev, curr, pitch, xb, xe, yb, ye, xcfl, ycfl); return 0;
@@ -77,10 +82,22 @@ CME_CPU_EXPORT int cme_cpu_heat_run_f64(double* a, double* b, int pitch, int xb,
 // FMA stencil variants (std::fma is correctly rounded).
 CME_CPU_EXPORT int cme_cpu_heat_step_fma_f32(const float* prev, float* curr, int pitch, int xb, int xe, int yb, int ye,
                                              int order, float xcfl, float ycfl) {
-    return heat_dispatch<float, true>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
+    return heat_dispatch<float, 1>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
 }
 
 CME_CPU_EXPORT int cme_cpu_heat_step_fma_f64(const double* prev, double* curr, int pitch, int xb, int xe, int yb,
                                              int ye, int order, double xcfl, double ycfl) {
-    return heat_dispatch<double, true>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
+    return heat_dispatch<double, 1>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
+}
+
+// Reassociated oracle (heat_update_fast): bitwise reference for the GPU's
+// "fast" stencil variants.
+CME_CPU_EXPORT int cme_cpu_heat_step_fast_f32(const float* prev, float* curr, int pitch, int xb, int xe, int yb,
+                                              int ye, int order, float xcfl, float ycfl) {
+    return heat_dispatch<float, 2>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
+}
+
+CME_CPU_EXPORT int cme_cpu_heat_step_fast_f64(const double* prev, double* curr, int pitch, int xb, int xe, int yb,
+                                              int ye, int order, double xcfl, double ycfl) {
+    return heat_dispatch<double, 2>(prev, curr, pitch, xb, xe, yb, ye, order, xcfl, ycfl);
 }

@@ -14,6 +14,11 @@
 
 using namespace cme;
 
+// a wave-uniform float moved to an SGPR (usable as the scalar operand of VALU ops)
+__device__ __forceinline__ float uniform_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 // ---------------------------------------------------------------- pipe
 // Wave-pipelined temporal blocking: NS (2..6) timesteps per HBM pass with the
 // steps split ACROSS the waves of a workgroup instead of stacked in one wave.
@@ -43,7 +48,7 @@ using namespace cme;
 // are the centre rows of phase q+1 (needs RB == B), which the neighbour wave
 // reads back as the `old` operand of its DPP shifts (the lane with no DPP
 // source keeps it). Three edge buffers, one barrier per phase.
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT, int WPR = 1>
+template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR = 1>
 struct PipeN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
@@ -64,6 +69,7 @@ struct PipeN {
     bool out_lane, full_vec;
     int y0, y1, xb, xe, xb1, xe1, yb1, ye1;
     T xcfl, ycfl;
+    HeatFast<ORDER, T> fc;  // FMA >= 2 (3: capped at 4 waves/SIMD): folded weights, wave-uniform
     int r0, q;
 
     __device__ __forceinline__ const T* row_ptr(int r) const {
@@ -105,7 +111,11 @@ struct PipeN {
                 ym[k] = w[(s_lo + B - (k + 1)) % NW][j];
                 yp[k] = w[(s_lo + B + (k + 1)) % NW][j];
             }
-            const T u = heat_update_sel<ORDER, FMA>(c[j], xm, xp, ym, yp, xcfl, ycfl);
+            T u;
+            if constexpr (FMA >= 2)
+                u = heat_update_fast<ORDER>(c[j], xm, xp, ym, yp, fc);
+            else
+                u = heat_update_sel<ORDER, FMA != 0>(c[j], xm, xp, ym, yp, xcfl, ycfl);
             if constexpr (MASK) {
                 const int x = xbase + j;
                 o[j] = (row_in && x >= xb1 && x < xe1) ? u : c[j];
@@ -232,7 +242,7 @@ struct PipeN {
     }
 };
 
-template <typename T, int ORDER, int RB, int NS, bool FMA, bool CHECK, int PD, bool NT, int WPR>
+template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR>
 __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64 * WPR], V4<T> (*edge)[3][RB][WPR][2], int k,
                                           int sub, const T* src, T* dst, int pitch, int gy, int xbase, int lane,
                                           bool out_lane, bool full_vec, int y0, int y1, int xb, int xe, int xb1,
@@ -260,12 +270,21 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64 * WPR], V4<T> 
     st.ye1 = ye1;
     st.xcfl = xcfl;
     st.ycfl = ycfl;
+    if constexpr (FMA >= 2) {
+        const HeatFast<ORDER, T> f = heat_fast_coefs<ORDER>(xcfl, ycfl);
+        st.fc.c0 = uniform_f(f.c0);
+#pragma unroll
+        for (int i = 0; i < HeatOrder<ORDER>::B; ++i) {
+            st.fc.ax[i] = uniform_f(f.ax[i]);
+            st.fc.ay[i] = uniform_f(f.ay[i]);
+        }
+    }
     st.run_role(k);
 }
 
 // one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for streamN
-template <typename T, int ORDER, int RB, int NS, bool FMA, int PD = 1, bool NT = false, int WPR = 1>
-__global__ __launch_bounds__(NS * WPR * 64) void heat_pipe_kernel(const T* __restrict__ prev, T* __restrict__ curr,
+template <typename T, int ORDER, int RB, int NS, int FMA, int PD = 1, bool NT = false, int WPR = 1>
+__global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_pipe_kernel(const T* __restrict__ prev, T* __restrict__ curr,
                                                                   int pitch, int gy, S2Regions R, int xb1, int xe1,
                                                                   int yb1, int ye1, T xcfl, T ycfl) {
     static_assert(NS >= 2 && NS <= 6, "pipe: 2..6 steps per pass");
@@ -351,7 +370,7 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
     return ((chunk + RB - 1) / RB) * RB;
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int RB, int PD = 1, bool NT = false, int WPR = 1>
+template <typename T, int ORDER, int NS, int FMA, int RB, int PD = 1, bool NT = false, int WPR = 1>
 int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl, T ycfl,
                       int chunk_hint, int per_cu, hipStream_t s) {
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
@@ -437,6 +456,16 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
             if constexpr (RB == 4)
                 return launch_pipe_multi<float, 8, NS, true, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
                                                                          per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 12:  // depth 1, non-temporal stores, reassociated ("fast") arithmetic
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, 2, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
+                                                                      per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 13:  // the same, registers capped for 4 waves per SIMD
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, 3, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
+                                                                      per_cu, s);
             return (int)hipErrorInvalidValue;
         case 21:  // + two waves per role (seams through LDS)
             if constexpr (RB == 4)

@@ -153,6 +153,51 @@ def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
         assert torch.equal(out.cpu(), oracle[ns]), (ns, pd, pc, ch)
 
 
+def _fast_steps(c, region, ns):
+    """ns steps of the reassociated CPU oracle (cme_cpu_heat_step_fast_f32)."""
+    from cme213x import _ext
+    a, b = c.buf[0].clone(), c.buf[0].clone()
+    for _ in range(ns):
+        _ext.call_cpu("cme_cpu_heat_step_fast_f32", a.data_ptr(), b.data_ptr(), c.pitch, *region, 8, c.xcfl, c.ycfl)
+        a, b = b, a
+    return a
+
+
+def test_fast_oracle_close_to_exact():
+    """The reassociated ("fast") stencil is the same FTCS update: within a few
+    ULP of the exact oracle over 8 steps (the reference's criterion is 10)."""
+    from cme213x.ops.stencil import heat_run
+    from cme213x.utils.ulp import ulp_distance
+    p = SimParams(nx=300, ny=250, order=8)
+    c = _rand_grid(p, torch.float32, seed=7)
+    region = c.interior
+    fast = _fast_steps(c, region, 8)
+    ca, cb = c.buf[0].clone(), c.buf[0].clone()
+    exact = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, 8, "naive")
+    assert not torch.equal(fast, exact)
+    assert int(ulp_distance(fast.numpy(), exact.numpy()).max()) <= 10
+
+
+@pytest.mark.gpu
+def test_gpu_pipe_fast_arms_bitwise(gpu):
+    """The reassociated-arithmetic tuning arms (pd 12: default registers, 13:
+    capped at 4 waves/SIMD) equal ns steps of the CPU fast oracle bit for bit."""
+    from cme213x import _ext
+    p = SimParams(nx=1500, ny=700, order=8)
+    c = _rand_grid(p, torch.float32, seed=9)
+    g = _rand_grid(p, torch.float32, gpu, seed=9)
+    region = (9, 1400, 6, 690)
+    s = _ext.stream_ptr(g.buf[0].device)
+    for ns in (3, 4):
+        oracle = _fast_steps(c, region, ns)
+        for pd in (12, 13):
+            out = g.buf[0].clone()
+            _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, *region,
+                          g.xcfl, g.ycfl, 0, 4, ns, pd, 0, s)
+            torch.cuda.synchronize()
+            assert torch.equal(out.cpu(), oracle), (ns, pd)
+
+
 @pytest.mark.gpu
 def test_gpu_pipe_long_run_matches_streamn(gpu):
     """A 16384-wide, 2048-row strip (one rank's share of an 8-GPU run) over 24
