@@ -57,8 +57,15 @@ _PRED = {"flags": 0, "neq": 1, "head": 2}
 _TILE = 4096  # kTile in algorithms.hip
 
 
+# GPU select algorithm for values / indices: "rts" (reduce-then-scan, two
+# reads of the input; default, faster at 2^26) or "lookback" (one pass with a
+# two-level decoupled look-back; csrc/hip/algorithms.hip select_lookback_kernel)
+SELECT_ALGO = "rts"
+
+
 def _select_ws_bytes(n: int) -> int:  # = cme_select_ws_bytes
-    return 8 * ((n + _TILE - 1) // _TILE) + 4096 + 64
+    t = (n + _TILE - 1) // _TILE
+    return 16 * t + 16 * ((t + 63) // 64) + 4096 + 64
 
 
 _ws: dict = {}
@@ -103,11 +110,18 @@ def _select(x: torch.Tensor, flags: torch.Tensor | None, pred: str, value=0, inv
                       _PRED[pred], _bits(x, value) if pred == "neq" else 0, int(invert), mode, out.data_ptr(),
                       ctypes.addressof(cnt))
         return out, cnt.value
+    from .scan import _check_lookback
+
+    lookback = SELECT_ALGO == "lookback" and mode != 2
     cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
     ws = _workspace(x.device, _select_ws_bytes(n))
+    if lookback:
+        _check_lookback(x, before=True)
     _ext.call_hip("cme_select", x.data_ptr(), flags.data_ptr() if flags is not None else None, n, _esize(x),
-                  _PRED[pred], _bits(x, value) if pred == "neq" else 0, int(invert), mode, out.data_ptr(),
-                  cnt.data_ptr(), ws.data_ptr(), _ext.stream_ptr(x.device))
+                  _PRED[pred], _bits(x, value) if pred == "neq" else 0, int(invert), mode | (8 if lookback else 0),
+                  out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), _ext.stream_ptr(x.device))
+    if lookback:
+        _check_lookback(x)
     return out, int(cnt.item())
 
 

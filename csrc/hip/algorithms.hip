@@ -4,11 +4,15 @@
 // native wave64 kernels.
 //
 //  select      : copy_if / remove_copy_if / unique / stable_partition /
-//                nonzero-indices. Reduce-then-scan, deterministic and stable:
+//                nonzero-indices, deterministic and stable. Reduce-then-scan:
 //                (1) per-4096-tile selected counts from the predicate,
 //                (2) exclusive scan of tile counts (cme_scan_rts),
 //                (3) per-tile block scan, selected items compacted in LDS,
 //                    then written as one contiguous coalesced run per tile.
+//                Alternative for values / indices: ONE pass with the tile's
+//                output offset from a two-level decoupled look-back over the
+//                selected counts (select_lookback_kernel; slower, see
+//                select_impl).
 //                Predicates: flags[i] != 0, x[i] != value, i == 0 ||
 //                x[i] != x[i-1] (head of a run: unique / reduce_by_key keys);
 //                optionally inverted. Output: the values, or their indices.
@@ -20,6 +24,7 @@
 //  inner       : inner_product with (plus, multiplies) in fp32 with a fp64
 //                per-lane accumulator, or (plus, equal_to) counting matches.
 #include "cme213/common.h"
+#include "cme213/lookback.h"
 #include "cme213/wave.h"
 
 using namespace cme;
@@ -34,6 +39,7 @@ constexpr int kTile = kThreads * kItems;
 
 // predicate codes
 enum : int { kPredFlags = 0, kPredNeq = 1, kPredHead = 2 };
+constexpr int kSelectLookback = 8;  // cme_select mode bit: single-pass look-back (modes 0 / 1)
 
 template <typename U>
 __device__ __forceinline__ bool pred_at(const U* __restrict__ x, const uint8_t* __restrict__ flags, long long i, int pred,
@@ -169,6 +175,110 @@ __global__ __launch_bounds__(kThreads) void select_scatter_kernel(const U* __res
         for (int k = tile_sel + threadIdx.x; k < tile_len; k += kThreads) o[uns_off + (k - tile_sel)] = stage[k];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *count_out = total_sel;
+}
+
+// Single-pass select (modes 0 values / 1 indices): block b compacts tiles b,
+// b+G, ... in order; the tile's output offset is the exclusive prefix of the
+// selected counts, resolved by the two-level decoupled look-back (wave 0,
+// lookback.h lb2_lookback) while the other waves stage the selected items in
+// LDS. The next tile's raw items (full aligned tiles) are loaded before the
+// look-back wait, so a block keeps two tiles of loads in flight. Reads the
+// input once (the reduce-then-scan path reads it twice).
+template <typename U>
+struct RawTile {
+    U v[kItems];
+    uint4 fw;  // kPredFlags: the 16 flag bytes
+    U prev;    // kPredHead: the item before this thread's first
+};
+
+template <typename U>
+__device__ __forceinline__ void raw_load(const U* __restrict__ x, const uint8_t* __restrict__ flags, long long base,
+                                         int pred, RawTile<U>& r) {
+    const uint4* px = reinterpret_cast<const uint4*>(x + base);
+#pragma unroll
+    for (int k = 0; k < (int)(kItems * sizeof(U) / 16); ++k) {
+        const uint4 w = px[k];
+        __builtin_memcpy(reinterpret_cast<char*>(r.v) + 16 * k, &w, 16);
+    }
+    if (pred == kPredFlags) r.fw = *reinterpret_cast<const uint4*>(flags + base);
+    if (pred == kPredHead) r.prev = base > 0 ? x[base - 1] : U(0);
+}
+
+template <typename U>
+__device__ __forceinline__ uint32_t raw_mask(const RawTile<U>& r, long long base, int pred, U value, int invert) {
+    uint32_t mask = 0;
+    if (pred == kPredFlags) {
+        uint8_t f[kItems];
+        __builtin_memcpy(f, &r.fw, 16);
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) mask |= (uint32_t)(f[j] != 0) << j;
+    } else if (pred == kPredNeq) {
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) mask |= (uint32_t)(r.v[j] != value) << j;
+    } else {
+        mask |= (uint32_t)(base == 0 || r.v[0] != r.prev);
+#pragma unroll
+        for (int j = 1; j < kItems; ++j) mask |= (uint32_t)(r.v[j] != r.v[j - 1]) << j;
+    }
+    return invert ? (~mask & 0xffffu) : mask;
+}
+
+template <typename U, int MODE>
+__global__ __launch_bounds__(kThreads) void select_lookback_kernel(const U* __restrict__ x,
+                                                                   const uint8_t* __restrict__ flags, long long n,
+                                                                   int pred, U value, int invert, int ntiles,
+                                                                   uint64_t* desc, unsigned* timeout,
+                                                                   void* __restrict__ out,
+                                                                   long long* __restrict__ count_out) {
+    using O = typename std::conditional<MODE == 1, long long, U>::type;
+    __shared__ O stage[kTile];
+    __shared__ int red[kThreads / kWave];
+    __shared__ int s_pre;
+    const int lane = lane_id();
+    const int wid = threadIdx.x / kWave;
+    const Lb2 lbv = lb2_views(desc, ntiles);
+    O* o = reinterpret_cast<O*>(out);
+    const void* fl_chk = pred == kPredFlags ? (const void*)flags : nullptr;
+    RawTile<U> cur, nxt;
+    int tile = blockIdx.x;
+    if (tile < ntiles && tile_vec_ok(x, fl_chk, n, (long long)tile * kTile))
+        raw_load<U>(x, flags, (long long)tile * kTile + (long long)threadIdx.x * kItems, pred, cur);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const long long tile0 = (long long)tile * kTile;
+        const long long base = tile0 + (long long)threadIdx.x * kItems;
+        uint32_t mask;
+        if (tile_vec_ok(x, fl_chk, n, tile0)) {
+            mask = raw_mask<U>(cur, base, pred, value, invert);
+        } else {
+            mask = load_items<U>(x, flags, n, base, pred, value, invert, false, cur.v);
+        }
+        int tile_sel;
+        const int off = block_exclusive_scan<kThreads / kWave>(__builtin_popcount(mask), red, tile_sel);
+        if (threadIdx.x == 0) lb2_put(lbv.agg + tile, tile_sel);
+        int ks = off;
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            if (mask >> j & 1u) {
+                if constexpr (MODE == 1)
+                    stage[ks++] = (O)(base + j);
+                else
+                    stage[ks++] = cur.v[j];
+            }
+        }
+        const int next = tile + gridDim.x;
+        if (next < ntiles && tile_vec_ok(x, fl_chk, n, (long long)next * kTile))
+            raw_load<U>(x, flags, (long long)next * kTile + (long long)threadIdx.x * kItems, pred, nxt);
+        if (wid == 0) {
+            const int pre = lb2_lookback<int>(lbv, tile, ntiles, tile_sel, 0u, timeout);
+            if (lane == 0) s_pre = pre;
+        }
+        __syncthreads();
+        const long long sel_off = s_pre;
+        for (int k = threadIdx.x; k < tile_sel; k += kThreads) o[sel_off + k] = stage[k];
+        if (tile == ntiles - 1 && threadIdx.x == 0) *count_out = sel_off + tile_sel;
+        __syncthreads();  // stage and s_pre are rewritten by the next tile
+        cur = nxt;
+    }
 }
 
 template <typename T, bool UPPER>
@@ -358,6 +468,32 @@ int select_impl(const U* x, const uint8_t* flags, long long n, int pred, U value
     if (n <= 0) return (int)hipMemsetAsync(count_out, 0, sizeof(long long), s);
     const long long ntiles = cdiv(n, (long long)kTile);
     if (ntiles > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    // mode | kSelectLookback (modes 0 / 1): the single-pass look-back kernel.
+    // Measured at 2^26 (benchmarks/bench_primitives.py, profiles/
+    // select_lookback_r2.jsonl): 0.209 ms vs 0.126 for reduce-then-scan --
+    // 16384 tiles of 4096 items are 16 rounds of the persistent grid, and
+    // each round pays the look-back hand-off; reduce-then-scan stays default.
+    const bool lookback = (mode & kSelectLookback) != 0;
+    mode &= ~kSelectLookback;
+    if (lookback && mode == 2) return (int)hipErrorInvalidValue;
+    if (lookback) {
+        if (ntiles > 0x3fffffffLL) return (int)hipErrorInvalidValue;
+        unsigned* timeout = lb_host_timeout();
+        if (!timeout) return (int)hipErrorOutOfMemory;
+        static const int bpc0 = persistent_blocks_per_cu(select_lookback_kernel<U, 0>, kThreads);
+        static const int bpc1 = persistent_blocks_per_cu(select_lookback_kernel<U, 1>, kThreads);
+        const long long cap = (long long)device_cu_count() * (mode == 0 ? bpc0 : bpc1);
+        const int grid = (int)(ntiles < cap ? ntiles : cap);
+        uint64_t* desc = lb_descriptors(ws);
+        CME_TRY(hipMemsetAsync(ws, 0, lb2_ws_bytes(ntiles), s));  // cme_select_ws_bytes covers it
+        if (mode == 0)
+            hipLaunchKernelGGL((select_lookback_kernel<U, 0>), dim3(grid), dim3(kThreads), 0, s, x, flags, n, pred,
+                               value, invert, (int)ntiles, desc, timeout, out, count_out);
+        else
+            hipLaunchKernelGGL((select_lookback_kernel<U, 1>), dim3(grid), dim3(kThreads), 0, s, x, flags, n, pred,
+                               value, invert, (int)ntiles, desc, timeout, out, count_out);
+        CME_LAUNCH_STATUS();
+    }
     int* counts = ws;
     int* offsets = ws + ntiles;
     void* scan_ws = ws + 2 * ntiles;
@@ -436,12 +572,17 @@ int arg_impl(const T* x, long long n, void* ws, T* ov, long long* oi, hipStream_
 
 }  // namespace
 
-// Workspace for cme_select: ints for 2 * tiles + the tile-count scan scratch.
-CME_EXPORT long long cme_select_ws_bytes(long long n) { return 8 * cdiv(n, (long long)kTile) + 4096 + 64; }
+// Workspace for cme_select: ints for 2 * tiles + the tile-count scan scratch,
+// or the two-level look-back descriptors (lb2_ws_bytes), whichever is larger.
+CME_EXPORT long long cme_select_ws_bytes(long long n) {
+    const long long t = cdiv(n, (long long)kTile);
+    return 16 * t + 16 * cdiv(t, 64LL) + 4096 + 64;
+}
 
 // esize: 1, 4 or 8 bytes per element (values compared bitwise).
 // pred: 0 flags!=0, 1 x!=value, 2 head-of-run; mode: 0 values, 1 indices,
-// 2 stable partition. *count_out (device) = number selected.
+// 2 stable partition; + 8: single-pass look-back kernel (modes 0 / 1).
+// *count_out (device) = number selected.
 CME_EXPORT int cme_select(const void* x, const uint8_t* flags, long long n, int esize, int pred,
                           unsigned long long value, int invert, int mode, void* out, long long* count_out, void* ws,
                           void* stream) {
@@ -516,6 +657,7 @@ CME_EXPORT int cme_inner_product(const void* a, const void* b, long long n, int 
 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(select_scatter_u32, 256, select_scatter_kernel<uint32_t, 0>);
+CME_REGISTER_KERNEL(select_lookback_u32, 256, select_lookback_kernel<uint32_t, 0>);
 CME_REGISTER_KERNEL(search_i32, 256, search_kernel<int, false>);
 CME_REGISTER_KERNEL(search2_i32, 256, search2_kernel<int, false, 4096>);
 CME_REGISTER_KERNEL(arg_partial_f32, 256, arg_partial_kernel<float, true>);

@@ -54,6 +54,25 @@ def test_select_family_gpu(gpu, n, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 4097, 100_003, 3 * (1 << 22) + 5])
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float64])
+def test_select_lookback_gpu(gpu, dtype, n, monkeypatch):
+    """The single-pass look-back select (values, indices, unique; 12.6M items
+    = ~3000 tiles = several rounds of the persistent grid) equals the CPU
+    backend."""
+    monkeypatch.setattr(A, "SELECT_ALGO", "lookback")
+    x = _data(n, dtype, hi=1000)
+    fl = _data(n, torch.int32, seed=2, hi=5) != 0
+    xg, fg = x.to(gpu), fl.to(gpu)
+    assert torch.equal(A.copy_if(xg, fg).cpu(), A.copy_if(x, fl))
+    assert torch.equal(A.nonzero(fg).cpu(), A.nonzero(fl))
+    xs = torch.sort(x).values
+    assert torch.equal(A.unique(xs.to(gpu)).cpu(), A.unique(xs))
+    from cme213x.ops.scan import lookback_timed_out
+    assert not lookback_timed_out(gpu)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32, torch.float64, torch.int64, torch.uint32])
 @pytest.mark.parametrize("upper", [False, True])
 @pytest.mark.parametrize("m", [70_000, 300_000])  # 300K queries take the two-level splitter kernel
