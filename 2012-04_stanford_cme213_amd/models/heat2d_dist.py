@@ -430,6 +430,19 @@ class DistHeat:
         if int(st["flags"][_IPC_TIMEOUT_WORD].item()) != 0:
             raise RuntimeError("IPC halo exchange timed out waiting for a peer; state is invalid")
 
+    def gate_check(self) -> None:
+        """Raise if a border workgroup of the fused native schedule
+        (CME_DIST_SCHEDULE=2) stopped waiting for a halo exchange that never
+        signalled (bounded in-kernel wait; the state is then invalid)."""
+        import ctypes
+
+        from .. import _ext
+
+        t = ctypes.c_int(0)
+        _ext.call_hip("cme_heat_dist_gate_status", ctypes.addressof(t))
+        if t.value:
+            raise RuntimeError("fused native schedule: a border wait for the halo exchange timed out; state is invalid")
+
     def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None,
                    ipc=None) -> None:
         """``iters`` timesteps in ONE native call (``cme_heat_dist_run``):

@@ -37,6 +37,7 @@
 #include <string>
 
 #include "cme213/common.h"
+#include "cme213/heat_region.h"
 
 extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream);
@@ -48,6 +49,10 @@ extern "C" int cme_heat_stepn_f32(const float* prev, float* curr, int pitch, int
 extern "C" int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
                                  const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
                                  void* stream);
+extern "C" int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                       const int* ext, int order, int nsteps, float xcfl, float ycfl, int fma,
+                                       int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+                                       void* stream);
 extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
@@ -522,6 +527,11 @@ struct SubCtx {
     hipStream_t compute = nullptr, border = nullptr, comm = nullptr;
     hipEvent_t ev_border[2] = {nullptr, nullptr}, ev_int[2] = {nullptr, nullptr}, ev_comm = nullptr;
     hipEvent_t ev_start = nullptr, ev_pack = nullptr;
+    // fused schedule: the comm stream signals xflag = ++xposted after each
+    // exchange; the next pass's border workgroups wait for it in-kernel
+    unsigned* xflag = nullptr;     // device word
+    unsigned xposted = 0;          // last value signalled (host mirror)
+    unsigned* xtimeout = nullptr;  // pinned host word: a gated wait gave up
 };
 
 struct DistCtx {
@@ -565,6 +575,11 @@ int get_ctx(int nsub, DistCtx** out) {
         CME_TRY(hipEventCreateWithFlags(&u.ev_comm, evf));
         CME_TRY(hipEventCreateWithFlags(&u.ev_start, evf));
         CME_TRY(hipEventCreateWithFlags(&u.ev_pack, evf));
+        CME_TRY(hipMalloc(&u.xflag, sizeof(unsigned)));
+        CME_TRY(hipMemset(u.xflag, 0, sizeof(unsigned)));
+        CME_TRY(hipHostMalloc(&u.xtimeout, sizeof(unsigned), hipHostMallocMapped));
+        *u.xtimeout = 0u;
+        u.xposted = 0;
     }
     if (nsub > c.nsub) c.nsub = nsub;
     *out = &c;
@@ -741,14 +756,23 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
     if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
-    // 0 (default): border stream || interior stream; 1: border then interior
-    // on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
+    // 2 (default, see `fused` below) where it applies, else 0: border stream
+    // || interior stream; 1: border then interior on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for
     // re-measuring on other topologies.
     static const int schedule = [] {
         const char* e = getenv("CME_DIST_SCHEDULE");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 2;
     }();
+    // 2 (fused): ONE pipelined launch per pass holding the deep interior and
+    // the border strips; the border workgroups (last in the grid) wait
+    // in-kernel for the previous exchange's flag, so the compute queue never
+    // waits on another queue (each such cross-queue wait cost ~14 us per
+    // pass at N = 8, profiles/dist_fused_r2.md). fp32 pipelined passes, one
+    // subdomain per process; other configurations use schedule 0.
+    const bool fused = schedule == 2 && !sync && nsub == 1 && sizeof(T) == 4 && (fma & kKernelPipe) &&
+                       tblock >= 3 && transport != 1 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions &&
+                       subs[0].n_int >= 1;
     DistCtx* ctx;
     CME_TRY_INT(get_ctx(nsub, &ctx));
     const ncclDataType_t dt = sizeof(T) == 4 ? ncclFloat32 : ncclFloat64;
@@ -851,7 +875,33 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         // fewer steps reuses the tblock*B-deep halos and regions)
         const int ns = (iters - it) < tblock ? (iters - it) : tblock;
         const int par = pass & 1;
-        if (sync) {
+        if (fused) {
+            SubCtx& u = ctx->sub[0];
+            const SubDesc& d = subs[0];
+            if (ns >= 3) {  // deep interior first (no wait), border strips gated on the last exchange
+                int regs[4 * cme::kMaxS2Regions];
+                for (int i = 0; i < 4 * d.n_int; ++i) regs[i] = d.interior[i];
+                for (int i = 0; i < 4 * d.n_b; ++i) regs[4 * d.n_int + i] = d.border[i];
+                CME_TRY_INT(cme_heat_pipe_gated_f32((const float*)d.buf[cur], (float*)d.buf[cur ^ 1], d.pitch, d.gy,
+                                                    regs, d.n_int + d.n_b, d.ext, order, ns, (float)xcfl,
+                                                    (float)ycfl, fma & 1, d.n_int, u.xflag, u.xposted, u.xtimeout,
+                                                    (void*)u.compute));
+            } else {  // tail pass on the non-pipelined kernels: plain stream order
+                CME_TRY_INT(wait_if(u.compute, u.ev_comm, comm_rec));
+                CME_TRY_INT(sweep(0, d.interior, d.n_int, cur, ns, u.compute));
+                CME_TRY_INT(sweep(0, d.border, d.n_b, cur, ns, u.compute));
+            }
+            CME_TRY(hipEventRecord(u.ev_int[par], u.compute));
+            int_rec[par] = true;
+            CME_TRY(hipStreamWaitEvent(u.comm, u.ev_int[par], 0));
+            CME_TRY_INT(exchange_all(cur ^ 1));
+            FlagList fl;
+            fl.n = 1;
+            fl.f[0] = u.xflag;
+            CME_TRY_INT(launch_signal(fl, ++u.xposted, u.comm));
+            CME_TRY(hipEventRecord(u.ev_comm, u.comm));
+            comm_rec = true;
+        } else if (sync) {
             for (int si = 0; si < nsub; ++si) {
                 SubCtx& u = ctx->sub[si];
                 CME_TRY_INT(sweep(si, subs[si].interior, subs[si].n_int, cur, ns, u.compute));
@@ -942,6 +992,21 @@ CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, in
                                sync, exchange_first, tblock, fma, cur_out, as_stream(stream));
     return dist_run<double>(transport, (ncclComm_t)comm, sd, nsub, order, xcfl, ycfl, iters, cur, sync,
                             exchange_first, tblock, fma, cur_out, as_stream(stream));
+}
+
+// Fused-schedule health: *timed_out = 1 if a gated border wait of the native
+// loop on this device gave up since the last call (the state is then
+// invalid); clears the words. Synchronises the device first.
+CME_EXPORT int cme_heat_dist_gate_status(int* timed_out) {
+    *timed_out = 0;
+    DistCtx* ctx;
+    CME_TRY_INT(get_ctx(0, &ctx));
+    CME_TRY(hipDeviceSynchronize());
+    for (int i = 0; i < ctx->nsub; ++i) {
+        if (ctx->sub[i].xtimeout && *ctx->sub[i].xtimeout) *timed_out = 1;
+        if (ctx->sub[i].xtimeout) *ctx->sub[i].xtimeout = 0u;
+    }
+    return 0;
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)

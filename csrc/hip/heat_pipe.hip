@@ -284,9 +284,9 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][64 * WPR], V4<T> 
 
 // one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for streamN
 template <typename T, int ORDER, int RB, int NS, int FMA, int PD = 1, bool NT = false, int WPR = 1>
-__global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_pipe_kernel(const T* __restrict__ prev, T* __restrict__ curr,
-                                                                  int pitch, int gy, S2Regions R, int xb1, int xe1,
-                                                                  int yb1, int ye1, T xcfl, T ycfl) {
+__global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_pipe_kernel(
+    const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
+    int ye1, T xcfl, T ycfl, PipeGate gate) {
     static_assert(NS >= 2 && NS <= 6, "pipe: 2..6 steps per pass");
     __shared__ V4<T> ring[NS - 1][2][RB][64 * WPR];
     __shared__ V4<T> edge[WPR > 1 ? NS : 1][3][RB][WPR][2];
@@ -301,6 +301,21 @@ __global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_
     int r = 0;
     while (task >= R.wave_end[r]) ++r;
     if (r > 0) task -= R.wave_end[r - 1];
+    if (gate.flag && r >= gate.from) {  // border strips of the fused schedule: halos of the previous exchange
+        if (threadIdx.x == 0 && __hip_atomic_load(gate.timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+            for (unsigned spins = 0;; ++spins) {
+                const unsigned v = __hip_atomic_load(gate.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((int)(v - gate.val) >= 0) break;
+                if (spins >= (1u << 22)) {
+                    __hip_atomic_store(gate.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the halo rows the exchange wrote, not stale L1 lines
+    }
     const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
     const int strips = R.strips[r], chunk = R.chunk[r];
     const int strip = task % strips;
@@ -343,6 +358,10 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
         const char* e = getenv("CME_PIPE_PER_CU");
         return e ? atoi(e) : 0;
     }();
+    static const int thin_min = [] {
+        const char* e = getenv("CME_PIPE_THIN_MIN");
+        return e ? atoi(e) : 64;
+    }();
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
         const int per_cu = per_cu_hint > 0 ? per_cu_hint : env_per_cu;
@@ -350,7 +369,15 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
         const long lo = 4 * RB > 16 ? 4 * RB : 16;
         long rows;
         if ((long)strips * cdiv(H, lo) < 1024) {
+            // thin regions (a distributed subdomain's border strips): every
+            // chunk pays 2(NS-1)B warm-up + (NS-1)RB fill rows, so chunks are
+            // at least thin_min rows (or the whole height) -- 4-row chunks
+            // made the 16-row border strips of an N = 8 rank cost 10x their
+            // rows, running 85 us beside the interior (profiles/
+            // dist_border_chunk_r2.md)
             rows = ((long)strips * H + 1023) / 1024;
+            rows = rows < thin_min ? thin_min : rows;
+            rows = rows > H ? H : rows;
             rows = rows < RB ? RB : rows;
         } else {
             // default: two rounds unless that cuts chunks below 128 rows
@@ -372,7 +399,7 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
 
 template <typename T, int ORDER, int NS, int FMA, int RB, int PD = 1, bool NT = false, int WPR = 1>
 int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl, T ycfl,
-                      int chunk_hint, int per_cu, hipStream_t s) {
+                      int chunk_hint, int per_cu, hipStream_t s, PipeGate gate = PipeGate{}) {
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
     static const long resident = [] {
@@ -384,9 +411,12 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
     }();
     S2Regions R{};
     int tasks = 0;
+    const int gate_from = gate.from;
+    gate.from = kMaxS2Regions;  // region index in R of the first gated input region
     for (int i = 0; i < n; ++i) {
         const Region& g = gs[i];
         const int H = g.ye - g.yb;
+        if (i >= gate_from && gate.from == kMaxS2Regions) gate.from = R.n;
         if (H <= 0 || g.xe <= g.xb) continue;
         const int strips = (int)cdiv(g.xe - (g.xb & ~3), PipeOut<NS, WPR>::kOut);
         const int chunk = pipe_chunk<NS, RB>(strips, H, chunk_hint, per_cu, resident);
@@ -399,7 +429,7 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
     }
     if (R.n == 0) return 0;
     hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR>), dim3(tasks), dim3(NS * WPR * 64), 0, s,
-                       prev, curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl);
+                       prev, curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl, gate);
     CME_LAUNCH_STATUS();
 }
 
@@ -411,20 +441,20 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
 namespace {
 template <int ORDER, bool FMA>
 int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, float xcfl,
-            float ycfl, int chunk, hipStream_t s) {
+            float ycfl, int chunk, hipStream_t s, PipeGate gate) {
     switch (ns) {
-        case 3: return launch_pipe_multi<float, ORDER, 3, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
-        case 4: return launch_pipe_multi<float, ORDER, 4, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
+        case 3: return launch_pipe_multi<float, ORDER, 3, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+        case 4: return launch_pipe_multi<float, ORDER, 4, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }
 template <bool FMA>
 int pipe_order(int order, const float* p, float* c, int pitch, int gy, const Region* gs, int n, Region e, int ns,
-               float xcfl, float ycfl, int chunk, hipStream_t s) {
+               float xcfl, float ycfl, int chunk, hipStream_t s, PipeGate gate = PipeGate{}) {
     switch (order) {
-        case 2: return pipe_ns<2, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
-        case 4: return pipe_ns<4, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
-        case 8: return pipe_ns<8, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 2: return pipe_ns<2, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
+        case 4: return pipe_ns<4, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
+        case 8: return pipe_ns<8, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -441,6 +471,28 @@ CME_EXPORT int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int 
                                   as_stream(stream))
                : pipe_order<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, chunk,
                                    as_stream(stream));
+}
+
+// The same pass with regions [wait_from, nout) gated on *flag >= value (the
+// fused distributed schedule: deep interior and border strips in ONE launch,
+// the border workgroups waiting for the previous halo exchange).
+CME_EXPORT int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                       const int* ext, int order, int nsteps, float xcfl, float ycfl, int fma,
+                                       int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+                                       void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions || (flag && !timeout)) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    PipeGate gate;
+    gate.flag = flag;
+    gate.val = value;
+    gate.from = wait_from;
+    gate.timeout = timeout;
+    return fma ? pipe_order<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0, as_stream(stream),
+                                  gate)
+               : pipe_order<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
+                                   as_stream(stream), gate);
 }
 
 // Tuning entry for the wave-pipelined NS-step pass (order 8, FMA): ns 3..6,

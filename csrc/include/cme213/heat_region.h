@@ -11,10 +11,11 @@ struct Region {
     int xb, xe, yb, ye;
 };
 
-// Up to four output regions per launch (a distributed subdomain's border
-// strips go out as ONE launch); every region shares the intermediate-step
-// region passed next to it.
-constexpr int kMaxS2Regions = 4;
+// Up to eight output regions per launch (a distributed subdomain's border
+// strips go out as ONE launch, or its deep interior AND border strips in the
+// fused schedule); every region shares the intermediate-step region passed
+// next to it.
+constexpr int kMaxS2Regions = 8;
 struct S2Regions {
     int n;
     int xb[kMaxS2Regions], xe[kMaxS2Regions], yb[kMaxS2Regions], ye[kMaxS2Regions];
@@ -34,6 +35,18 @@ struct StripN {
 template <int NS, int WPR>
 struct PipeOut {
     static constexpr int kOut = (64 * WPR - 2 * NS) * 4;
+};
+
+// Fused-schedule gate of the pipelined pass: workgroups of regions
+// [from, n) wait until *flag >= val (wrap-safe) before reading their input
+// -- the halo exchange of the previous pass signals the flag from the comm
+// stream (dist_heat.hip). Bounded: a wait past the spin limit sets *timeout
+// (pinned host word) and proceeds. flag == nullptr: no gate.
+struct PipeGate {
+    const unsigned* flag = nullptr;
+    unsigned val = 0;
+    int from = 0;
+    unsigned* timeout = nullptr;
 };
 
 }  // namespace cme
