@@ -82,6 +82,7 @@ def native_selftest(comm, native, dev, args) -> bool:
         raise TimeoutError("native loop self-test did not finish within 60 s")
     if args.transport == "ipc":
         a.ipc_check()
+    a.gate_check()  # fused schedule: no border wait gave up on the exchange
     for _ in range(6):
         b.step()
     b.finish()
@@ -261,6 +262,8 @@ def main() -> int:
         native.check()  # surface asynchronous RCCL failures instead of reporting a number
     elif use_native:
         sim.ipc_check()  # a wait that gave up on a peer invalidates the run
+    if use_native:
+        sim.gate_check()  # ... as does a fused-schedule border wait that gave up
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     comm.allreduce_(elapsed, "max")
     secs = float(elapsed.item())

@@ -303,14 +303,20 @@ __global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_
     if (r > 0) task -= R.wave_end[r - 1];
     if (gate.flag && r >= gate.from) {  // border strips of the fused schedule: halos of the previous exchange
         if (threadIdx.x == 0 && __hip_atomic_load(gate.timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+            // ~2^24 polls (tens of seconds: an exchange that includes RCCL's
+            // first-use connection setup must not trip it); sticky -- once one
+            // workgroup gives up, the others stop at their next check
             for (unsigned spins = 0;; ++spins) {
                 const unsigned v = __hip_atomic_load(gate.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((int)(v - gate.val) >= 0) break;
-                if (spins >= (1u << 22)) {
+                if (spins >= (1u << 24)) {
                     __hip_atomic_store(gate.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(4);
+                if ((spins & 1023u) == 1023u &&
+                    __hip_atomic_load(gate.timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+                    break;
+                __builtin_amdgcn_s_sleep(8);
             }
         }
         __syncthreads();

@@ -153,6 +153,33 @@ def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
         assert torch.equal(out.cpu(), oracle[ns]), (ns, pd, pc, ch)
 
 
+@pytest.mark.gpu
+def test_gpu_pipe_gated_regions(gpu):
+    """The fused-schedule entry (cme_heat_pipe_gated_f32): deep interior plus
+    gated border strips in one launch, gate already open, equals the plain
+    pipelined pass over the same regions."""
+    import ctypes
+
+    from cme213x import _ext
+    from cme213x.ops.stencil import heat_stepn
+    p = SimParams(nx=600, ny=500, order=8)
+    g = _rand_grid(p, torch.float32, gpu, seed=4)
+    regs = [(4, 604, 40, 464), (4, 604, 4, 40), (4, 604, 464, 504)]  # interior, then two border strips
+    ext = (4, 604, 4, 504)
+    ref = g.buf[0].clone()
+    heat_stepn(g.buf[0], ref, regs, ext, 8, g.xcfl, g.ycfl, 4, fma=True, kernel="pipe")
+    flag = torch.full((1,), 7, dtype=torch.int32, device=gpu)
+    tw = torch.zeros(1, dtype=torch.int32, device=gpu)  # the timeout word must be device-visible
+    flat = (ctypes.c_int * 12)(*[v for r in regs for v in r])
+    e = (ctypes.c_int * 4)(*ext)
+    out = g.buf[0].clone()
+    _ext.call_hip("cme_heat_pipe_gated_f32", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy,
+                  ctypes.addressof(flat), 3, ctypes.addressof(e), 8, 4, g.xcfl, g.ycfl, 1, 1, flag.data_ptr(), 7,
+                  tw.data_ptr(), _ext.stream_ptr(g.buf[0].device))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and int(tw.item()) == 0
+
+
 def _fast_steps(c, region, ns):
     """ns steps of the reassociated CPU oracle (cme_cpu_heat_step_fast_f32)."""
     from cme213x import _ext
