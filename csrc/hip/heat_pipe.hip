@@ -380,22 +380,22 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
             // at least thin_min rows (or the whole height) -- 4-row chunks
             // made the 16-row border strips of an N = 8 rank cost 10x their
             // rows, running 85 us beside the interior (profiles/
-            // dist_border_chunk_r2.md)
+            // dist_fused_r2.md)
             rows = ((long)strips * H + 1023) / 1024;
             rows = rows < thin_min ? thin_min : rows;
             rows = rows > H ? H : rows;
             rows = rows < RB ? RB : rows;
         } else {
-            // default: two rounds unless that cuts chunks below 128 rows
-            // (benchmarks/tune_heat_pipe.py, profiles/heat_pipe_r2.md: 2
-            // rounds win at H >= 4096 rows, one round at 2048)
-            rows = 0;
-            for (int r = per_cu > 0 ? 1 : 2; r >= 1; --r) {
-                long per_strip = r * target / strips;
-                per_strip = per_strip < 1 ? 1 : per_strip;
-                rows = (H + per_strip - 1) / per_strip;
-                if (rows >= 128) break;
-            }
+            // default, measured on the bench's field (benchmarks/
+            // tune_heat_pipe.py, profiles/heat_pipe_chunk_r2.md): 14 tasks
+            // per CU for tall regions (>= 8192 rows: ~340 / 170-row chunks
+            // at 16384 / 8192 rows), 8 at >= 4096 rows, one round of the
+            // resident workgroups below that (2048 rows: ~100-row chunks)
+            long tasks = target;
+            if (per_cu <= 0) tasks = H >= 8192 ? 14L * device_cu_count() : (H >= 4096 ? 8L * device_cu_count() : resident);
+            long per_strip = tasks / strips;
+            per_strip = per_strip < 1 ? 1 : per_strip;
+            rows = (H + per_strip - 1) / per_strip;
             rows = rows < lo ? lo : rows;
         }
         chunk = (int)rows;
