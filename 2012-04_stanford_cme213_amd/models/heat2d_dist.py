@@ -150,12 +150,10 @@ class DistHeat:
             raise ValueError("multi-process runs own exactly one subdomain per rank")
         if tblock not in (1, 2, 3, 4):
             raise ValueError("tblock must be 1..4")
-        if tblock > 3 and dtype == torch.float64 and torch.device(device).type == "cuda":
-            raise ValueError("tblock 4 (4-step passes) is fp32 only on the GPU")
         if kernel not in ("streamn", "pipe"):
             raise ValueError("kernel must be 'streamn' or 'pipe'")
-        if kernel == "pipe" and dtype == torch.float64 and tblock > 2 and torch.device(device).type == "cuda":
-            raise ValueError("the pipelined pass is fp32 only")
+        if tblock > 3 and dtype == torch.float64 and kernel != "pipe" and torch.device(device).type == "cuda":
+            raise ValueError("fp64 4-step passes need kernel='pipe' on the GPU (streamN fp64 stops at 3)")
         self.fma = bool(fma)
         # 3-4 step passes: streamN (one wave holds every step) or the
         # wave-pipelined kernel (csrc/hip/heat_pipe.hip); identical results

@@ -23,6 +23,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiipipiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f32", "ppiipipiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f64", "ppiipipiiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f32", "ppiipipiiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f64", "ppiipipiiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
@@ -43,10 +44,10 @@ VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_no
 # variants that advance more than one timestep per launch (multi-step drivers
 # only); stream4 (4 steps per HBM pass) is fp32 only, stream3 takes fp32 and
 # fp64 (one row per register block for doubles); pipeN = the wave-pipelined
-# N-step pass (csrc/hip/heat_pipe.hip), fp32
+# N-step pass (csrc/hip/heat_pipe.hip), fp32 and fp64
 MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma", "pipe3", "pipe3_fma",
              "pipe4", "pipe4_fma"}
-FP32_ONLY = {"stream4", "stream4_fma", "pipe3", "pipe3_fma", "pipe4", "pipe4_fma"}
+FP32_ONLY = {"stream4", "stream4_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
 FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma"}
@@ -115,8 +116,8 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
     (nsteps-1)*B cells, e.g. into an nsteps*B-deep halo), the last one writes
     ``curr`` on every region of ``regions`` (one tuple or a list of <= 4, one
     launch). Cells of ``ext`` outside the grid's update set keep their value.
-    Bitwise equal to ``nsteps`` single steps; 4 steps are fp32 only.
-    ``kernel="pipe"`` (fp32, 3 or 4 steps) runs the wave-pipelined pass
+    Bitwise equal to ``nsteps`` single steps; fp64 4-step passes need
+    ``kernel="pipe"``. ``kernel="pipe"`` (3 or 4 steps) runs the wave-pipelined pass
     (csrc/hip/heat_pipe.hip) instead of streamN: same cells, same bits.
     On CPU it runs exactly those single steps through temporaries."""
     if kernel not in ("streamn", "pipe"):
@@ -143,17 +144,15 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
             heat_step(src, curr, reg, order, xcfl, ycfl, v)
         return
     f64 = prev.dtype == torch.float64
-    if f64 and nsteps > 3:
-        raise ValueError("4-step passes are fp32 only")
+    if f64 and nsteps > 3 and kernel != "pipe":
+        raise ValueError("fp64 4-step passes need kernel='pipe'")
     rows, pitch = prev.shape
     flat = [int(v) for reg in regions for v in reg]
     r = (ctypes.c_int * len(flat))(*flat)
     e = (ctypes.c_int * 4)(*map(int, ext))
     name = "cme_heat_stepn_f64" if f64 else "cme_heat_stepn_f32"
     if kernel == "pipe" and nsteps >= 3:
-        if f64:
-            raise ValueError("the pipelined pass is fp32 only")
-        name = "cme_heat_pipe_f32"
+        name = "cme_heat_pipe_f64" if f64 else "cme_heat_pipe_f32"
     _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), len(regions),
                   ctypes.addressof(e), order, nsteps, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
 

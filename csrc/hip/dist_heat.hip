@@ -53,6 +53,9 @@ extern "C" int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch
                                        const int* ext, int order, int nsteps, float xcfl, float ycfl, int fma,
                                        int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
                                        void* stream);
+extern "C" int cme_heat_pipe_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                 const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
+                                 void* stream);
 extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
@@ -423,6 +426,8 @@ int stepn_regions<float>(const float* p, float* c, int pitch, int gy, const int*
 template <>
 int stepn_regions<double>(const double* p, double* c, int pitch, int gy, const int* r, int n, const int* ext,
                           int order, int ns, double xcfl, double ycfl, int fma, hipStream_t s) {
+    if ((fma & kKernelPipe) && ns >= 3)
+        return cme_heat_pipe_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
     return cme_heat_stepn_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
 }
 
@@ -755,7 +760,8 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if ((transport == 0 || transport == 3) && nsub != 1) return (int)hipErrorInvalidValue;
     if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
-    if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4)) return (int)hipErrorInvalidValue;
+    if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4 && !(fma & kKernelPipe)))
+        return (int)hipErrorInvalidValue;
     // 2 (default, see `fused` below) where it applies, else 0: border stream
     // || interior stream; 1: border then interior on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for

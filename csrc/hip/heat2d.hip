@@ -751,7 +751,10 @@ namespace {
 
 }  // namespace
 
-// heat_pipe.hip: the wave-pipelined NS-step pass (variants 11-14, fp32)
+// heat_pipe.hip: the wave-pipelined NS-step pass (variants 11-14)
+extern "C" int cme_heat_pipe_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                 const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
+                                 void* stream);
 extern "C" int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
                                  const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk, int fma,
                                  void* stream);
@@ -804,13 +807,13 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         }
     } else if (variant >= 11 && variant <= 14) {
         // wave-pipelined NS = 3 (11 exact, 12 FMA) / 4 (13, 14) steps per pass
-        if constexpr (sizeof(T) == 4) {
-            const int r[4] = {g.xb, g.xe, g.yb, g.ye};
+        const int r[4] = {g.xb, g.xe, g.yb, g.ye};
+        if constexpr (sizeof(T) == 4)
             return cme_heat_pipe_f32(prev, curr, pitch, gy, r, 1, r, ORDER, variant <= 12 ? 3 : 4, xcfl, ycfl,
                                      chunk_hint, (variant & 1) ? 0 : 1, s);
-        } else {
-            return (int)hipErrorInvalidValue;
-        }
+        else
+            return cme_heat_pipe_f64(prev, curr, pitch, gy, r, 1, r, ORDER, variant <= 12 ? 3 : 4, xcfl, ycfl,
+                                     chunk_hint, (variant & 1) ? 0 : 1, s);
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -977,7 +980,8 @@ CME_EXPORT int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, i
 // variant: 0 naive, 1 lds(+1 pad), 2 stream, 3 lds(no pad), 4 stream2 (TWO
 // steps), 5 stream2 FMA (TWO steps), 6 stream FMA, 7 / 8 stream3 exact / FMA
 // (THREE steps, fp32), 9 / 10 stream4 exact / FMA (FOUR steps, fp32),
-// 11 / 12 pipe3 exact / FMA, 13 / 14 pipe4 exact / FMA (wave-pipelined, fp32)
+// 11 / 12 pipe3 exact / FMA, 13 / 14 pipe4 exact / FMA (wave-pipelined, fp32
+// and fp64)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -1003,7 +1007,7 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     T* bufs[2] = {a, b};
     int i = 0;
     if (variant >= 7 && variant <= 14) {
-        if (sizeof(T) != 4 && variant > 8) return (int)hipErrorInvalidValue;
+        if (sizeof(T) != 4 && (variant == 9 || variant == 10)) return (int)hipErrorInvalidValue;
         const int ns = (variant <= 8 || variant == 11 || variant == 12) ? 3 : 4;
         for (; i + ns <= iters; i += ns) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);

@@ -479,6 +479,44 @@ CME_EXPORT int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int 
                                    as_stream(stream));
 }
 
+// fp64: the same pass on doubles (32 B per lane per row; RB = 2 rows per
+// phase keeps the window + prefetch within ~128 VGPRs). The hw5 workload is
+// double precision (hw/hw5/2dHeat_solution.cpp:63-84).
+namespace {
+template <int ORDER, bool FMA>
+int pipe_ns_f64(const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, double xcfl,
+                double ycfl, int chunk, hipStream_t s) {
+    switch (ns) {
+        case 3: return launch_pipe_multi<double, ORDER, 3, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
+        case 4: return launch_pipe_multi<double, ORDER, 4, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+template <bool FMA>
+int pipe_order_f64(int order, const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e,
+                   int ns, double xcfl, double ycfl, int chunk, hipStream_t s) {
+    switch (order) {
+        case 2: return pipe_ns_f64<2, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 4: return pipe_ns_f64<4, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 8: return pipe_ns_f64<8, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_pipe_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                 const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
+                                 void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    return fma ? pipe_order_f64<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, chunk,
+                                      as_stream(stream))
+               : pipe_order_f64<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, chunk,
+                                       as_stream(stream));
+}
+
 // The same pass with regions [wait_from, nout) gated on *flag >= value (the
 // fused distributed schedule: deep interior and border strips in ONE launch,
 // the border workgroups waiting for the previous halo exchange).

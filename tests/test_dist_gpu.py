@@ -123,7 +123,8 @@ def test_native_loop_loopback_transport(gpu, method, world, sync, tblock, fma, d
 @pytest.mark.parametrize("sync", [False, True])
 @pytest.mark.parametrize("tblock,fma", [(3, False), (3, True), (4, False), (4, True)])
 @pytest.mark.parametrize("native", [True, False])
-def test_pipe_kernel_subdomains_gpu(gpu, method, world, sync, tblock, fma, native):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_pipe_kernel_subdomains_gpu(gpu, method, world, sync, tblock, fma, native, dtype):
     """The wave-pipelined 3-4 step pass (csrc/hip/heat_pipe.hip) on the
     distributed schedule -- deep interior, border strips in one launch,
     intermediate steps into the nB-deep halos -- through the native loop
@@ -134,15 +135,15 @@ def test_pipe_kernel_subdomains_gpu(gpu, method, world, sync, tblock, fma, nativ
 
     p = SimParams(nx=333, ny=270, order=8, iters=9, sync=sync, grid_method=method, ic=5.0,
                   bc=(1.0, 10.0, 3.0, 7.0), flavor="hw5")
-    ref = DistHeat(p, None, torch.float32, "cpu", variant="naive", fma=fma)
-    sim = DistHeat(p, None, torch.float32, gpu, local_ranks=list(range(world)), world=world, tblock=tblock, fma=fma,
+    ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)
+    sim = DistHeat(p, None, dtype, gpu, local_ranks=list(range(world)), world=world, tblock=tblock, fma=fma,
                    kernel="pipe")
     for d in (ref, sim):
         for s in d.subs.values():
             g, b = s.grid, s.blk
             H = g.H
             yy, xx = np.meshgrid(np.arange(b.ny) + b.y0, np.arange(b.nx) + b.x0, indexing="ij")
-            ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0).to(torch.float32)
+            ic = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0).to(dtype)
             g.buf[:, H:H + b.ny, H:H + b.nx] = ic.to(g.device)
         d.exchange(d._cur()).wait()
     ref.run(p.iters)
