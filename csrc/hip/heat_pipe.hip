@@ -355,7 +355,7 @@ __global__ __launch_bounds__(NS * WPR * 64, (FMA == 3 ? 16 / NS : 1)) void heat_
 // (border strips) use ~1024 tasks. CME_PIPE_CHUNK / CME_PIPE_PER_CU override
 // for sweeps (per_cu = task target per CU).
 template <int NS, int RB>
-int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident) {
+int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident, bool thin_floor) {
     static const int env_chunk = [] {
         const char* e = getenv("CME_PIPE_CHUNK");
         return e ? atoi(e) : 0;
@@ -381,9 +381,13 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
             // made the 16-row border strips of an N = 8 rank cost 10x their
             // rows, running 85 us beside the interior (profiles/
             // dist_fused_r2.md)
+            // (multi-region launches only: a lone small region -- a whole
+            // 1000^2 grid -- is latency-bound and wants many short chunks)
             rows = ((long)strips * H + 1023) / 1024;
-            rows = rows < thin_min ? thin_min : rows;
-            rows = rows > H ? H : rows;
+            if (thin_floor) {
+                rows = rows < thin_min ? thin_min : rows;
+                rows = rows > H ? H : rows;
+            }
             rows = rows < RB ? RB : rows;
         } else {
             // default, measured on the bench's field (benchmarks/
@@ -425,7 +429,7 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         if (i >= gate_from && gate.from == kMaxS2Regions) gate.from = R.n;
         if (H <= 0 || g.xe <= g.xb) continue;
         const int strips = (int)cdiv(g.xe - (g.xb & ~3), PipeOut<NS, WPR>::kOut);
-        const int chunk = pipe_chunk<NS, RB>(strips, H, chunk_hint, per_cu, resident);
+        const int chunk = pipe_chunk<NS, RB>(strips, H, chunk_hint, per_cu, resident, n > 1);
         const int k = R.n++;
         R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
         R.strips[k] = strips;
