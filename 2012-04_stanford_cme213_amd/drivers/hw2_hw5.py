@@ -34,7 +34,11 @@ def heat2d_mpi_main(argv=None) -> int:
     ap.add_argument("--ranks", type=int, default=0, help="simulate N ranks in one process (loopback)")
     ap.add_argument("--device", default=None)
     ap.add_argument("--float", action="store_true", help="fp32 instead of the reference's fp64")
+    ap.add_argument("--tblock", default="auto", help="timesteps per halo exchange / HBM pass (1-4, or auto)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "pipe", "streamn"], help="3-4 step pass kernel")
+    ap.add_argument("--fma", action="store_true", help="FMA-contracted stencil (the reference CPU's is not)")
     a = ap.parse_args(argv)
+    tblock = a.tblock if a.tblock == "auto" else int(a.tblock)
     dtype = torch.float32 if a.float else torch.float64
     if a.ranks:
         import time
@@ -42,7 +46,8 @@ def heat2d_mpi_main(argv=None) -> int:
         p = SimParams.from_file(a.params, flavor="hw5")
         print(p.banner())
         dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-        sim = DistHeat(p, None, dtype, dev, local_ranks=list(range(a.ranks)), world=a.ranks)
+        sim = DistHeat(p, None, dtype, dev, local_ranks=list(range(a.ranks)), world=a.ranks, tblock=tblock,
+                       fma=a.fma, kernel=a.kernel)
         sim.save_text("init")
         t0 = time.perf_counter()
         sim.run(p.iters)
@@ -53,5 +58,5 @@ def heat2d_mpi_main(argv=None) -> int:
         return 0
     comm = init_from_env()
     dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    run_hw5(a.params, comm, dtype, dev)
+    run_hw5(a.params, comm, dtype, dev, tblock=tblock, fma=a.fma, kernel=a.kernel)
     return 0

@@ -34,7 +34,7 @@ import time
 import numpy as np
 import torch
 
-from ..ops.stencil import heat_step, heat_stepn
+from ..ops.stencil import heat_run, heat_step, heat_stepn
 from ..parallel.comm import Comm, LoopbackComm, P2P, Pending
 from ..parallel.decomp import Block, decompose
 from ..utils.params import SimParams
@@ -133,6 +133,37 @@ class _Sub:
 
 _OPP = {"top": "bottom", "bottom": "top", "left": "right", "right": "left"}
 
+# fp64 subdomains at least this large run 3-4 step passes on the pipelined
+# kernel; smaller ones on streamN (measured, one MI355X, order 8, FMA:
+# 1000^2 stream3 0.0058 vs pipe4 0.0074 ms/iter; 2000^2 stream3 0.0096-0.0103
+# vs pipe4 0.0085 -- profiles/heat_fp64_pipe_r2.jsonl, heat_fp64_stream3_r2.jsonl,
+# dist_fused_r2.md)
+_F64_PIPE_MIN_POINTS = 2000 * 2000
+
+
+def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda") -> int:
+    """Timesteps per HBM pass (and per halo exchange) for a subdomain of
+    ``points`` cells: 4 for fp32 (pipelined pass, every N of the 16384^2
+    bench) and for large fp64 subdomains; 3 (FMA) or 2 (exact) for small fp64
+    ones, where streamN wins (exact fp64 1000^2: stream2 0.0073 vs stream3
+    0.0087 ms/iter). On the CPU backend: 1 (no temporal blocking)."""
+    if torch.device(device).type != "cuda":
+        return 1
+    if dtype == torch.float32 or points >= _F64_PIPE_MIN_POINTS:
+        return 4
+    return 3 if fma else 2
+
+
+def auto_kernel(dtype, points: int, tblock: int) -> str:
+    """Pass kernel for 3-4 step passes: the wave-pipelined pass for fp32 and
+    for fp64 subdomains of at least 2000^2 cells (and every fp64 4-step pass:
+    streamN stops at 3 for doubles), streamN below that."""
+    if tblock < 3:
+        return "streamn"
+    if dtype == torch.float32 or tblock > 3 or points >= _F64_PIPE_MIN_POINTS:
+        return "pipe"
+    return "streamn"
+
 
 class DistHeat:
     """Distributed heat solver. ``local_ranks`` lists the subdomains owned by
@@ -141,13 +172,20 @@ class DistHeat:
 
     def __init__(self, params: SimParams, comm: Comm | None = None, dtype=torch.float32, device="cpu",
                  local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream",
-                 tblock: int = 1, fma: bool = False, kernel: str = "streamn"):
+                 tblock: int | str = 1, fma: bool = False, kernel: str = "streamn"):
         self.p = params
         self.comm = comm or LoopbackComm()
         self.world = world or self.comm.size
         self.local_ranks = local_ranks if local_ranks is not None else [self.comm.rank]
         if self.comm.size > 1 and (len(self.local_ranks) != 1 or self.world != self.comm.size):
             raise ValueError("multi-process runs own exactly one subdomain per rank")
+        if tblock == "auto" or kernel == "auto":  # by the (largest) subdomain's size
+            pts = max(b.nx * b.ny for b in (decompose(params.nx, params.ny, self.world, params.grid_method, r)
+                                            for r in self.local_ranks))
+            if tblock == "auto":
+                tblock = auto_tblock(dtype, pts, fma, torch.device(device).type)
+            if kernel == "auto":
+                kernel = auto_kernel(dtype, pts, tblock)
         if tblock not in (1, 2, 3, 4):
             raise ValueError("tblock must be 1..4")
         if kernel not in ("streamn", "pipe"):
@@ -442,7 +480,7 @@ class DistHeat:
             raise RuntimeError("fused native schedule: a border wait for the halo exchange timed out; state is invalid")
 
     def run_native(self, iters: int, rccl=None, sync: bool | None = None, transport: int | None = None,
-                   ipc=None) -> None:
+                   ipc=None, fused: bool = True) -> None:
         """``iters`` timesteps in ONE native call (``cme_heat_dist_run``):
         border strips on their own stream, the halo exchange posted as soon
         as they finish, the deep interior overlapping both; with ``tblock=n``
@@ -451,7 +489,13 @@ class DistHeat:
         subdomain per process); ``None`` = loopback transport, every
         neighbour being another local subdomain (device copies) -- the same
         stream/event schedule, testable on one GPU. ``transport=2`` skips
-        the exchange (compute-schedule benchmarking only)."""
+        the exchange (compute-schedule benchmarking only). ``fused=False``
+        forbids the fused one-launch schedule for this call (schedule 0:
+        streams + events); the native loop also drops it by itself under
+        stream capture or when its queue-independence probe fails
+        (:meth:`schedule` reports what ran). Under ``CME_SYNC_CHECK`` every
+        call ends with :meth:`gate_check` / :meth:`ipc_check`, so a timed-out
+        in-kernel wait raises here instead of leaving a wrong state behind."""
         import ctypes
 
         from .. import _ext
@@ -470,12 +514,31 @@ class DistHeat:
         plan["subs"][0].ipc = ctypes.addressof(self._ipc_plan(ipc)["plan"]) if transport == 3 else None
         _ext.call_hip("cme_heat_dist_run", transport, rccl.handle if rccl is not None else None,
                       ctypes.addressof(plan["subs"]), len(self.subs), 0 if g0.dtype == torch.float32 else 1,
-                      g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock, self._flags(),
-                      ctypes.addressof(cur_out), _ext.stream_ptr(g0.device))
+                      g0.order, g0.xcfl, g0.ycfl, iters, g0.cur, int(sync), 0, self.tblock,
+                      self._flags() | (0 if fused else 4), ctypes.addressof(cur_out), _ext.stream_ptr(g0.device))
         for s in self.subs.values():
             s.grid.cur = cur_out.value
             s.grid.iteration += iters
         self.iteration += iters
+        if _ext.SYNC_CHECK:
+            self.gate_check()
+            if transport == 3:
+                self.ipc_check()
+
+    @staticmethod
+    def schedule() -> dict:
+        """What the last native run on this device used: ``schedule`` = "events"
+        (0: border / comm / interior streams), "one-stream" (1), "fused" (2:
+        one gated launch per pass), "sync" (3); ``probe`` = the fused
+        schedule's queue-independence probe ("passed" / "failed" /
+        "not run")."""
+        from .. import _ext
+
+        sch, probe = ctypes.c_int(-1), ctypes.c_int(0)
+        _ext.call_hip("cme_heat_dist_info", ctypes.addressof(sch), ctypes.addressof(probe))
+        names = {-1: "none", 0: "events", 1: "one-stream", 2: "fused", 3: "sync"}
+        return {"schedule": names.get(sch.value, str(sch.value)),
+                "probe": {1: "passed", -1: "failed"}.get(probe.value, "not run")}
 
     def finish(self) -> None:
         pend = getattr(self, "_pending", None)
@@ -483,7 +546,36 @@ class DistHeat:
             pend.wait()
             self._pending = None
 
+    def solo(self) -> bool:
+        """One GPU subdomain with no neighbour on any side (world 1): nothing
+        to exchange, so :meth:`run` hands the whole time loop to the native
+        multi-pass driver (``cme_heat_run_*``) -- one call, no per-pass Python."""
+        if self.device.type != "cuda" or len(self.subs) != 1:
+            return False
+        b = next(iter(self.subs.values())).blk
+        return b.top < 0 and b.bottom < 0 and b.left < 0 and b.right < 0
+
+    def run_variant(self) -> str:
+        """``heat_run`` variant with this solver's pass schedule: ``tblock``
+        steps per HBM pass on the chosen pass kernel, FMA or exact."""
+        if self.tblock == 1:
+            return self.variant
+        suffix = "_fma" if self.fma else ""
+        if self.tblock == 2:
+            return "stream2" + suffix
+        return ("pipe" if self.kernel == "pipe" else "stream") + str(self.tblock) + suffix
+
     def run(self, iters: int, sync: bool | None = None) -> None:
+        if self.solo():
+            self.finish()
+            s = next(iter(self.subs.values()))
+            g = s.grid
+            a, b = g.buf[g.cur], g.buf[1 - g.cur]
+            out = heat_run(a, b, g.interior, g.order, g.xcfl, g.ycfl, iters, self.run_variant())
+            g.cur = g.cur if out is a else 1 - g.cur
+            g.iteration += iters
+            self.iteration += iters
+            return
         i = 0
         while iters - i >= 2 and self.tblock >= 2:
             ns = min(self.tblock, iters - i)
@@ -618,14 +710,17 @@ def _ext_region(s: _Sub):
 
 
 def run_hw5(params_path: str, comm: Comm | None = None, dtype=torch.float64, device: str | None = None,
-            write_files: bool = True) -> dict:
-    """The hw5 driver (double precision, as the reference)."""
+            write_files: bool = True, tblock: int | str = "auto", fma: bool = False, kernel: str = "auto") -> dict:
+    """The hw5 driver (double precision, as the reference). On the GPU the
+    steps per pass and the pass kernel are chosen from the subdomain size
+    (:func:`auto_tblock`, :func:`auto_kernel`); ``fma=False`` keeps the
+    reference CPU's uncontracted arithmetic."""
     comm = comm or LoopbackComm()
     p = SimParams.from_file(params_path, flavor="hw5")
     if comm.rank == 0:
         print(p.banner())
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
-    sim = DistHeat(p, comm, dtype, device)
+    sim = DistHeat(p, comm, dtype, device, tblock=tblock, fma=fma, kernel=kernel)
     if write_files:
         sim.save_text("init")
     if sim.device.type == "cuda":

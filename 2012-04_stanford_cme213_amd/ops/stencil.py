@@ -29,6 +29,8 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_gate_status", "p")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_gated_f32", "ppiipipiiffiipupp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_gated_f64", "ppiipipiiddiipupp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_info", "pp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")

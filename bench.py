@@ -50,18 +50,23 @@ def _wait_bounded(dev, seconds: float) -> bool:
     return True
 
 
-def native_selftest(comm, native, dev, args) -> bool:
-    """Run a small problem through the native loop (RCCL or IPC transport)
-    AND the torch.distributed loop (the path the multi-process CPU tests
-    cover) and require bitwise-equal subdomains on every rank before trusting
-    the native loop for the measurement. A native run that does not finish
-    within 60 s counts as a failure (the caller aborts the communicator)."""
+def selftest(comm, native, dev, args, fused: bool = True) -> bool:
+    """Bitwise self-test of the timed path. A 1024^2 problem with a
+    non-uniform interior runs 2*tblock+1 timesteps (whole passes plus a tail)
+    along the EXACT path the timed loop takes -- the native multi-pass driver
+    at N = 1, the native loop (RCCL or IPC transport; ``fused`` = whether the
+    fused schedule may be used) at N > 1 -- and must equal, bit for bit on
+    every rank, the same number of single FMA steps of the torch.distributed
+    loop (the path the multi-process CPU tests cover). A native run that does
+    not finish within 60 s counts as a failure (the caller aborts the
+    communicator)."""
     import torch
 
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.utils.params import SimParams
 
-    p = SimParams(nx=1024, ny=1024, iters=6, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
+    iters = 2 * args.tblock + 1
+    p = SimParams(nx=1024, ny=1024, iters=iters, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
     a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma),
                  kernel=args.kernel)
@@ -74,16 +79,19 @@ def native_selftest(comm, native, dev, args) -> bool:
         xx = torch.arange(s.blk.nx, device=dev, dtype=torch.float32).view(1, -1) + s.blk.x0
         g.buf[:, B:B + s.blk.ny, B:B + s.blk.nx] = 5.0 + torch.sin(0.05 * xx) * torch.cos(0.03 * yy)
         sim.exchange(sim._cur()).wait()
-    if args.transport == "ipc":
-        a.run_native(6, ipc=native)
+    if native is None:
+        a.run(iters)
+    elif args.transport == "ipc":
+        a.run_native(iters, ipc=native, fused=fused)
     else:
-        a.run_native(6, native)
+        a.run_native(iters, native, fused=fused)
     if not _wait_bounded(dev, 60.0):
-        raise TimeoutError("native loop self-test did not finish within 60 s")
-    if args.transport == "ipc":
-        a.ipc_check()
-    a.gate_check()  # fused schedule: no border wait gave up on the exchange
-    for _ in range(6):
+        raise TimeoutError("self-test run did not finish within 60 s")
+    if native is not None:
+        if args.transport == "ipc":
+            a.ipc_check()
+        a.gate_check()  # fused schedule: no border wait gave up on the exchange
+    for _ in range(iters):
         b.step()
     b.finish()
     torch.cuda.synchronize(dev)
@@ -134,6 +142,9 @@ def main() -> int:
     ap.add_argument("--native", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: run the K-step loop in C++ over a native communicator (auto: after a "
                          "bitwise self-test against the torch.distributed loop)")
+    ap.add_argument("--schedule", choices=["auto", "events"], default="auto",
+                    help="native loop: auto = fused one-launch passes where the native loop allows them (falls back "
+                         "to events if the self-test fails); events = schedule 0 (border / comm / interior streams)")
     ap.add_argument("--transport", choices=["rccl", "ipc"], default="rccl",
                     help="native halo transport: rccl = grouped ncclSend/Recv; ipc = peers' memory mapped "
                          "with hipIpcOpenMemHandle, pulled by a kernel over xGMI")
@@ -181,6 +192,7 @@ def main() -> int:
         return bool(t.item() == 1.0)
 
     native, native_ok = None, False
+    fused = args.schedule == "auto"
     if on_gpu and comm.size > 1 and args.native != "off":
         # 1) every rank can load the native library -- agreed BEFORE any
         #    collective native setup, so no rank is left alone inside
@@ -204,7 +216,17 @@ def main() -> int:
                     from cme213x.parallel.rccl import NativeRccl
 
                     native = NativeRccl()
-                native_ok = native_selftest(comm, native, dev, args) if args.native == "auto" else True
+                if args.native == "auto":
+                    native_ok = selftest(comm, native, dev, args, fused=fused)
+                    if not agree(native_ok) and fused:
+                        # the fused gated schedule failed (or its probe refused
+                        # it on some rank): retry the native loop on schedule 0
+                        print(f"bench.py rank {rank}: fused native schedule failed the self-test; "
+                              "retrying with schedule 0", file=sys.stderr)
+                        fused = False
+                        native_ok = selftest(comm, native, dev, args, fused=False)
+                else:
+                    native_ok = True
             except Exception as e:  # noqa: BLE001 - reported, then the portable path runs
                 print(f"bench.py rank {rank}: native {args.transport} loop unavailable ({e}); "
                       "using torch.distributed", file=sys.stderr)
@@ -223,11 +245,16 @@ def main() -> int:
 
     def run(k):
         if use_native and args.transport == "ipc":
-            sim.run_native(k, ipc=native)
+            sim.run_native(k, ipc=native, fused=fused)
         elif use_native:
-            sim.run_native(k, native)
+            sim.run_native(k, native, fused=fused)
         else:
             sim.run(k)
+
+    # the timed path's bitwise self-test at N = 1 (N > 1: above, per transport)
+    selftest_ok = native_ok if use_native else None
+    if on_gpu and comm.size == 1:
+        selftest_ok = selftest(comm, None, dev, args)
 
     def barrier_sync():
         sync()
@@ -235,9 +262,17 @@ def main() -> int:
         sync()
 
     # spin-up: untimed passes on a scratch copy of the solver until `spinup`
-    # seconds have elapsed (rank 0 decides the count; all ranks run it)
+    # seconds have elapsed (rank 0 decides the count; all ranks run it).
+    # First, one run of every pass length (1..tblock steps) so every kernel
+    # the warmup/timed loops launch has been loaded: a first launch loads its
+    # code object (~5 ms with the GPU idle), after which the clocks take ~10 ms
+    # to recover -- the slow timed passes of a 20-step run (gpurun trace,
+    # profiles/bench_driver_cmd_r3.md)
     spin = 0
     if on_gpu and args.spinup > 0:
+        for k in range(1, args.tblock + 1):
+            run(k)
+            spin += k
         t_end = time.perf_counter() + args.spinup
         while True:
             run(args.tblock * 4)
@@ -274,6 +309,11 @@ def main() -> int:
     bad = torch.tensor([float(~torch.isfinite(st).all()) + float(st.abs().max() > 1e3)], device=dev)
     comm.allreduce_(bad, "max")
 
+    if use_native:
+        sch = DistHeat.schedule()
+        schedule = sch["schedule"] + ("" if sch["probe"] == "not run" else f" (queue probe {sch['probe']})")
+    else:
+        schedule = "python passes" if comm.size > 1 else "heat_run (one native call)"
     pts = args.n * args.n
     bpp = bytes_per_point(args.order, torch.float32)
     eff = pts * bpp * args.steps / secs / 1e9
@@ -309,12 +349,15 @@ def main() -> int:
                 "device": args.device,
                 "rehearsal_shared_gpu": bool(args.share_gpu),
                 "loop": f"native-{args.transport}" if use_native else ("torch.distributed" if comm.size > 1
-                                                                         else "single"),
+                                                                         else "single (native multi-pass)"),
+                "transport": (args.transport if use_native else ("torch.distributed" if comm.size > 1 else "none")),
+                "schedule": schedule,
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
             "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),
             "gpoints_per_s": round(pts * args.steps / secs / 1e9, 2),
             "sanity_ok": bool(bad.item() == 0),
+            "selftest": selftest_ok,
             "native_selftest": (native_ok if native is not None else None),
             "spinup_steps": spin,
         }

@@ -56,6 +56,10 @@ extern "C" int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch
 extern "C" int cme_heat_pipe_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                  const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                  void* stream);
+extern "C" int cme_heat_pipe_gated_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                       const int* ext, int order, int nsteps, double xcfl, double ycfl, int fma,
+                                       int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+                                       void* stream);
 extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
@@ -412,6 +416,9 @@ int step_region<double>(const double* p, double* c, int pitch, int gy, const int
 // FMA-contracted stencil; bit 1 (kKernelPipe): 3-4 step fp32 passes run the
 // wave-pipelined kernel (heat_pipe.hip) instead of streamN -- same bits.
 constexpr int kKernelPipe = 2;
+// bit 2 of the same flags word (cme_heat_dist_run only): never use the fused
+// schedule in this call (schedule 0 instead) -- the caller's fallback
+constexpr int kNoFused = 4;
 template <typename T>
 int stepn_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, int ns,
                   T xcfl, T ycfl, int fma, hipStream_t s);
@@ -429,6 +436,41 @@ int stepn_regions<double>(const double* p, double* c, int pitch, int gy, const i
     if ((fma & kKernelPipe) && ns >= 3)
         return cme_heat_pipe_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
     return cme_heat_stepn_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
+}
+
+// fused-schedule pass: every region in one pipelined launch, regions
+// [wait_from, n) gated on *flag >= value
+template <typename T>
+int gated_pass(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, int ns, T xcfl,
+               T ycfl, int fma, int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+               hipStream_t s) {
+    if constexpr (sizeof(T) == 4)
+        return cme_heat_pipe_gated_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, fma & 1, wait_from, flag,
+                                       value, timeout, (void*)s);
+    else
+        return cme_heat_pipe_gated_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, fma & 1, wait_from, flag,
+                                       value, timeout, (void*)s);
+}
+
+// Queue-independence probe of the fused schedule. Its border workgroups spin
+// INSIDE the compute stream's kernel until the comm stream's signal kernel
+// runs; that is only safe if the two streams sit on different hardware
+// queues (with GPU_MAX_HW_QUEUES or a stream count that makes HIP share a
+// queue, the signal would wait behind the spinning kernel). One wave on the
+// compute stream spins (bounded: ~0.2 s) on a fresh device word that a
+// signal kernel on the comm stream sets; it reports 1 (seen) or 2 (gave up).
+__global__ __launch_bounds__(64) void gate_probe_kernel(const unsigned* flag, unsigned value, unsigned* result) {
+    if (threadIdx.x != 0) return;
+    unsigned r = 2u;
+    for (unsigned spins = 0; spins < (1u << 20); ++spins) {
+        const unsigned v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)(v - value) >= 0) {
+            r = 1u;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    __hip_atomic_store(result, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------- distributed loop
@@ -537,11 +579,17 @@ struct SubCtx {
     unsigned* xflag = nullptr;     // device word
     unsigned xposted = 0;          // last value signalled (host mirror)
     unsigned* xtimeout = nullptr;  // pinned host word: a gated wait gave up
+    // queue-independence probe (gate_probe_kernel): 0 not run, 1 passed,
+    // -1 failed (compute and comm share a hardware queue: no fused schedule)
+    int probe = 0;
+    unsigned* probe_word = nullptr;    // device word the comm stream signals
+    unsigned* probe_result = nullptr;  // pinned host word the probe writes
 };
 
 struct DistCtx {
     int dev = -1;
     int nsub = 0;
+    int last_schedule = -1;  // schedule the last dist_run used (cme_heat_dist_info)
     SubCtx sub[kMaxSubs];
 };
 
@@ -585,6 +633,10 @@ int get_ctx(int nsub, DistCtx** out) {
         CME_TRY(hipHostMalloc(&u.xtimeout, sizeof(unsigned), hipHostMallocMapped));
         *u.xtimeout = 0u;
         u.xposted = 0;
+        CME_TRY(hipMalloc(&u.probe_word, sizeof(unsigned)));
+        CME_TRY(hipMemset(u.probe_word, 0, sizeof(unsigned)));
+        CME_TRY(hipHostMalloc(&u.probe_result, sizeof(unsigned), hipHostMallocMapped));
+        *u.probe_result = 0u;
     }
     if (nsub > c.nsub) c.nsub = nsub;
     *out = &c;
@@ -743,6 +795,31 @@ int local_peers(const SubDesc* subs, int nsub, int si, int* out) {
     return n;
 }
 
+// Run the queue-independence probe once per subdomain context (synchronises
+// the compute and comm streams, so it runs before this call queues anything;
+// never under stream capture). Returns 0 and sets u.probe.
+int run_gate_probe(SubCtx& u) {
+    if (u.probe != 0) return 0;
+    static const bool verbose = getenv("CME_DIST_VERBOSE") != nullptr;
+    *u.probe_result = 0u;
+    CME_TRY(hipMemsetAsync(u.probe_word, 0, sizeof(unsigned), u.compute));
+    CME_TRY(hipStreamSynchronize(u.compute));
+    hipLaunchKernelGGL(gate_probe_kernel, dim3(1), dim3(64), 0, u.compute, (const unsigned*)u.probe_word, 1u,
+                       u.probe_result);
+    CME_TRY(hipGetLastError());
+    FlagList fl;
+    fl.n = 1;
+    fl.f[0] = u.probe_word;
+    CME_TRY_INT(launch_signal(fl, 1u, u.comm));
+    CME_TRY(hipStreamSynchronize(u.comm));
+    CME_TRY(hipStreamSynchronize(u.compute));
+    u.probe = (*u.probe_result == 1u) ? 1 : -1;
+    if (u.probe < 0 || verbose)
+        fprintf(stderr, "cme213x dist_run: compute/comm queue probe %s%s\n", u.probe > 0 ? "passed" : "FAILED",
+                u.probe > 0 ? "" : " (streams share a hardware queue): fused schedule disabled, using schedule 0");
+    return 0;
+}
+
 // The time loop. Per pass i (1..tblock timesteps), for every sub:
 //   border stream : wait halos of p (own comm event, + pulling neighbours'
 //                   in loopback) and the previous interior; border strips;
@@ -759,6 +836,13 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if (nsub < 1 || nsub > kMaxSubs) return (int)hipErrorInvalidValue;
     if ((transport == 0 || transport == 3) && nsub != 1) return (int)hipErrorInvalidValue;
     if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    CME_TRY(hipStreamIsCapturing(s, &cap));
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    // IPC epochs are host counters baked into the wait / signal kernels: a
+    // captured IPC run would replay stale epochs (peers' staging read before
+    // it is packed) -- refused
+    if (capturing && transport == 3) return (int)hipErrorStreamCaptureUnsupported;
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
     if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4 && !(fma & kKernelPipe)))
         return (int)hipErrorInvalidValue;
@@ -774,13 +858,24 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     // the border strips; the border workgroups (last in the grid) wait
     // in-kernel for the previous exchange's flag, so the compute queue never
     // waits on another queue (each such cross-queue wait cost ~14 us per
-    // pass at N = 8, profiles/dist_fused_r2.md). fp32 pipelined passes, one
-    // subdomain per process; other configurations use schedule 0.
-    const bool fused = schedule == 2 && !sync && nsub == 1 && sizeof(T) == 4 && (fma & kKernelPipe) &&
-                       tblock >= 3 && transport != 1 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions &&
-                       subs[0].n_int >= 1;
+    // pass at N = 8, profiles/dist_fused_r2.md). Pipelined passes (fp32 or
+    // fp64), one subdomain per process, and only when
+    //  * the caller did not ask for schedule 0 (kNoFused bit of `fma`),
+    //  * the caller's stream is not being captured into a graph (the gate
+    //    target and the flag are host-side counters baked into the kernel
+    //    arguments: a replay would see stale flags as already reached),
+    //  * the queue-independence probe passed (run_gate_probe).
+    // Other configurations use schedule 0.
+    bool fused = schedule == 2 && !(fma & kNoFused) && !capturing && !sync && nsub == 1 && (fma & kKernelPipe) &&
+                 tblock >= 3 && transport != 1 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions &&
+                 subs[0].n_int >= 1;
     DistCtx* ctx;
     CME_TRY_INT(get_ctx(nsub, &ctx));
+    if (fused) {
+        CME_TRY_INT(run_gate_probe(ctx->sub[0]));
+        fused = ctx->sub[0].probe > 0;
+    }
+    ctx->last_schedule = fused ? 2 : (sync ? 3 : (schedule == 1 ? 1 : 0));
     const ncclDataType_t dt = sizeof(T) == 4 ? ncclFloat32 : ncclFloat64;
     int peers[kMaxSubs][16];
     int npeer[kMaxSubs];
@@ -888,10 +983,9 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
                 int regs[4 * cme::kMaxS2Regions];
                 for (int i = 0; i < 4 * d.n_int; ++i) regs[i] = d.interior[i];
                 for (int i = 0; i < 4 * d.n_b; ++i) regs[4 * d.n_int + i] = d.border[i];
-                CME_TRY_INT(cme_heat_pipe_gated_f32((const float*)d.buf[cur], (float*)d.buf[cur ^ 1], d.pitch, d.gy,
-                                                    regs, d.n_int + d.n_b, d.ext, order, ns, (float)xcfl,
-                                                    (float)ycfl, fma & 1, d.n_int, u.xflag, u.xposted, u.xtimeout,
-                                                    (void*)u.compute));
+                CME_TRY_INT(gated_pass<T>((const T*)d.buf[cur], (T*)d.buf[cur ^ 1], d.pitch, d.gy, regs,
+                                          d.n_int + d.n_b, d.ext, order, ns, xcfl, ycfl, fma, d.n_int, u.xflag,
+                                          u.xposted, u.xtimeout, u.compute));
             } else {  // tail pass on the non-pipelined kernels: plain stream order
                 CME_TRY_INT(wait_if(u.compute, u.ev_comm, comm_rec));
                 CME_TRY_INT(sweep(0, d.interior, d.n_int, cur, ns, u.compute));
@@ -998,6 +1092,18 @@ CME_EXPORT int cme_heat_dist_run(int transport, void* comm, const void* subs, in
                                sync, exchange_first, tblock, fma, cur_out, as_stream(stream));
     return dist_run<double>(transport, (ncclComm_t)comm, sd, nsub, order, xcfl, ycfl, iters, cur, sync,
                             exchange_first, tblock, fma, cur_out, as_stream(stream));
+}
+
+// Which schedule the last cme_heat_dist_run on this device used: 0 streams +
+// events, 1 one compute stream, 2 fused (gated one-launch passes), 3 sync;
+// -1 before any run. probe: the fused schedule's queue-independence probe of
+// subdomain 0 (0 not run, 1 passed, -1 failed).
+CME_EXPORT int cme_heat_dist_info(int* schedule, int* probe) {
+    DistCtx* ctx;
+    CME_TRY_INT(get_ctx(0, &ctx));
+    *schedule = ctx->last_schedule;
+    *probe = ctx->nsub > 0 ? ctx->sub[0].probe : 0;
+    return 0;
 }
 
 // Fused-schedule health: *timed_out = 1 if a gated border wait of the native

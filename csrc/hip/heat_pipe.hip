@@ -489,20 +489,20 @@ CME_EXPORT int cme_heat_pipe_f32(const float* prev, float* curr, int pitch, int 
 namespace {
 template <int ORDER, bool FMA>
 int pipe_ns_f64(const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, double xcfl,
-                double ycfl, int chunk, hipStream_t s) {
+                double ycfl, int chunk, hipStream_t s, PipeGate gate) {
     switch (ns) {
-        case 3: return launch_pipe_multi<double, ORDER, 3, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
-        case 4: return launch_pipe_multi<double, ORDER, 4, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s);
+        case 3: return launch_pipe_multi<double, ORDER, 3, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+        case 4: return launch_pipe_multi<double, ORDER, 4, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }
 template <bool FMA>
 int pipe_order_f64(int order, const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e,
-                   int ns, double xcfl, double ycfl, int chunk, hipStream_t s) {
+                   int ns, double xcfl, double ycfl, int chunk, hipStream_t s, PipeGate gate = PipeGate{}) {
     switch (order) {
-        case 2: return pipe_ns_f64<2, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
-        case 4: return pipe_ns_f64<4, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
-        case 8: return pipe_ns_f64<8, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s);
+        case 2: return pipe_ns_f64<2, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
+        case 4: return pipe_ns_f64<4, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
+        case 8: return pipe_ns_f64<8, FMA>(p, c, pitch, gy, gs, n, e, ns, xcfl, ycfl, chunk, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -541,6 +541,27 @@ CME_EXPORT int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch
                                   gate)
                : pipe_order<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
                                    as_stream(stream), gate);
+}
+
+// fp64 twin of cme_heat_pipe_gated_f32 (the fused schedule on the hw5
+// workload's doubles, hw/hw5/2dHeat_solution.cpp:63-84).
+CME_EXPORT int cme_heat_pipe_gated_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
+                                       const int* ext, int order, int nsteps, double xcfl, double ycfl, int fma,
+                                       int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+                                       void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions || (flag && !timeout)) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    PipeGate gate;
+    gate.flag = flag;
+    gate.val = value;
+    gate.from = wait_from;
+    gate.timeout = timeout;
+    return fma ? pipe_order_f64<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
+                                      as_stream(stream), gate)
+               : pipe_order_f64<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
+                                       as_stream(stream), gate);
 }
 
 // Tuning entry for the wave-pipelined NS-step pass (order 8, FMA): ns 3..6,

@@ -71,5 +71,22 @@ def test_bench_multirank_shared_gpu_ipc(gpu, nproc, extra):
     rank on cuda:0, gloo control plane, IPC halo transport."""
     rec = _launch_gpu(nproc, ["--share-gpu", *extra])
     assert rec["n_gpus"] == nproc and rec["sanity_ok"] is True
-    assert rec["native_selftest"] is True
+    assert rec["native_selftest"] is True and rec["selftest"] is True
     assert rec["config"]["loop"] == "native-ipc" and rec["config"]["rehearsal_shared_gpu"] is True
+    assert rec["config"]["transport"] == "ipc" and rec["config"]["schedule"].split()[0] in ("fused", "events")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_single_gpu_selftest(gpu):
+    """N = 1 (the driver's BENCH run): the timed path -- one native
+    multi-pass call per loop -- passes its bitwise self-test against single
+    FMA steps and names its schedule."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "9", "--warmup", "5", "--grid", "2048",
+           "--spinup", "0.05"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["selftest"] is True and rec["sanity_ok"] is True
+    assert rec["steps"] == 9 and rec["warmup"] == 5
+    assert rec["config"]["schedule"] and rec["config"]["transport"] == "none"

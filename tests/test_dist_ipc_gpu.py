@@ -27,6 +27,7 @@ CASES_2 = [
     (2, True, 3, True, "float32"),
     (1, False, 4, True, "float32", "pipe"),
     (2, True, 3, False, "float32", "pipe"),
+    (1, False, 4, True, "float64", "pipe"),  # fp64 fused gated schedule
 ]
 CASES_4 = [
     (2, False, 1, False, "float32"),
@@ -58,7 +59,7 @@ def _set_ic(sim, dtype):
     sim.exchange(sim._cur()).wait()
 
 
-def _ipc_rank(rank, world, cases):
+def _ipc_rank(rank, world, cases, extra_streams=0):
     import torch
 
     import cme213x  # noqa: F401
@@ -67,6 +68,12 @@ def _ipc_rank(rank, world, cases):
     from cme213x.parallel.ipc import NativeIpc
 
     torch.cuda.set_device(0)
+    # streams created before the native loop's own: with more streams than
+    # hardware queues HIP maps several streams onto one queue
+    keep = []
+    lo, hi = torch.cuda.Stream.priority_range()
+    for prio in sorted({lo, hi}):
+        keep += [torch.cuda.Stream(priority=prio) for _ in range(extra_streams)]
     comm = TorchComm()
     out = []
     for method, sync, tblock, fma, dt, *kern in cases:
@@ -81,15 +88,15 @@ def _ipc_rank(rank, world, cases):
         s = next(iter(sim.subs.values()))
         H = s.grid.H
         own = s.grid.buf[s.grid.cur, H:H + s.blk.ny, H:H + s.blk.nx].cpu().numpy()
-        out.append((s.blk.x0, s.blk.y0, own))
+        out.append((s.blk.x0, s.blk.y0, own, DistHeat.schedule()))
         ipc.close()
     return out
 
 
-def _check(world, cases):
+def _check(world, cases, extra_streams=0):
     from cme213x.models.heat2d_dist import DistHeat
 
-    parts = run_ranks(_ipc_rank, world, (cases,), timeout=240)
+    parts = run_ranks(_ipc_rank, world, (cases, extra_streams), timeout=240)
     for ci, (method, sync, tblock, fma, dt, *_) in enumerate(cases):
         dtype = getattr(torch, dt)
         p = _params(method, sync)
@@ -99,10 +106,13 @@ def _check(world, cases):
         st = ref.gather_global()
         B = p.border
         for r in range(world):
-            x0, y0, own = parts[r][ci]
+            x0, y0, own, sch = parts[r][ci]
             want = st[B + y0:B + y0 + own.shape[0], B + x0:B + x0 + own.shape[1]]
             assert np.array_equal(own.astype(np.float64), want), \
-                f"case {cases[ci]} rank {r}: max |diff| {np.abs(own - want).max()}"
+                f"case {cases[ci]} rank {r} ({sch}): max |diff| {np.abs(own - want).max()}"
+            # the fused schedule only ever runs after its queue probe passed
+            assert sch["schedule"] != "fused" or sch["probe"] == "passed", sch
+    return parts
 
 
 @pytest.mark.gpu
@@ -115,6 +125,29 @@ def test_ipc_two_processes_one_gpu(gpu):
 @pytest.mark.timeout(300)
 def test_ipc_four_processes_one_gpu(gpu):
     _check(4, CASES_4)
+
+
+# fused-schedule cases (async, pipelined 4-step passes): fp32 and fp64
+_FUSED = [(1, False, 4, True, "float32", "pipe"), (1, False, 4, True, "float64", "pipe")]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("queues,extra_streams", [("1", 0), ("", 8)])
+def test_ipc_fused_under_hw_queue_sharing(gpu, monkeypatch, queues, extra_streams):
+    """The fused schedule's border workgroups spin in-kernel on a flag that
+    the comm stream's kernels set. With GPU_MAX_HW_QUEUES=1 in the rank
+    processes (set before their first GPU call), or 8 extra streams of each
+    priority created first, compute and comm may share a hardware queue;
+    the native loop's probe must then pick schedule 0 (or the fused run must
+    still be correct) -- bitwise against the single-grid oracle either way."""
+    if queues:
+        monkeypatch.setenv("GPU_MAX_HW_QUEUES", queues)
+    parts = _check(2, _FUSED, extra_streams)
+    if queues == "1":  # one queue per process: every stream shares it
+        for r in parts:
+            for *_, sch in r:
+                assert sch["schedule"] == "events" and sch["probe"] == "failed", sch
 
 
 def _spmv_rank(rank, world):
