@@ -257,7 +257,7 @@ def test_native_loop_graph_capture_replays(gpu, dtype):
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.utils.params import SimParams
 
-    p = SimParams(nx=700, ny=533, order=8, iters=8, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0), flavor="hw5")
+    p = SimParams(nx=700, ny=533, order=8, iters=8, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0), sync=False, flavor="hw5")
 
     def make():
         sim = DistHeat(p, None, dtype, gpu, tblock=4, fma=True, kernel="pipe")
