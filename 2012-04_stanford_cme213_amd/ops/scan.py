@@ -93,33 +93,38 @@ def _run_ws(x: torch.Tensor) -> torch.Tensor:
 
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_ws_bytes", "qp")
 _ext.proto(_ext.HIP_PROTOS, "cme_lookback_timeout_word", "p")
-_timeout_word = None
+_timeout_words: dict = {}
 
 
-def _tw():
-    """The look-back give-up word: pinned host memory the kernels store to
-    (lookback.h), readable without a device synchronisation."""
-    global _timeout_word
-    if _timeout_word is None:
-        import ctypes
+def _tw(device: torch.device | str | None = None):
+    """The look-back give-up word of ``device`` (default: the current one):
+    pinned host memory the kernels store to (lookback.h), one word per
+    device, readable without a device synchronisation."""
+    import ctypes
 
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    w = _timeout_words.get(idx)
+    if w is None:
         p = ctypes.c_void_p()
-        _ext.call_hip("cme_lookback_timeout_word", ctypes.addressof(p))
-        _timeout_word = ctypes.c_uint.from_address(p.value)
-    return _timeout_word
+        with torch.cuda.device(idx):
+            _ext.call_hip("cme_lookback_timeout_word", ctypes.addressof(p))
+        w = ctypes.c_uint.from_address(p.value)
+        _timeout_words[idx] = w
+    return w
 
 
 def lookback_timed_out(device: torch.device | str = "cuda") -> bool:
     """True if a look-back launch on ``device`` (since the last check) hit its
     bounded-spin limit -- its result is wrong. Synchronises the device."""
     torch.cuda.synchronize(torch.device(device))
-    return _tw().value != 0
+    return _tw(device).value != 0
 
 
 def check_lookback(device: torch.device | str = "cuda") -> None:
     """Synchronise and raise if any look-back launch gave up (then clear)."""
     if lookback_timed_out(device):
-        _tw().value = 0
+        _tw(device).value = 0
         raise RuntimeError("look-back scan spin limit exceeded: a result since the last check is invalid")
 
 
@@ -127,7 +132,7 @@ def _check_lookback(x: torch.Tensor, before: bool = False) -> None:
     """Called around every look-back launch. Before one: the give-up word of
     EARLIER launches is read without a sync (it is sticky host memory) and
     raised. After one: only under CME_SYNC_CHECK (which synchronises)."""
-    w = _tw()
+    w = _tw(x.device)
     if before:
         if w.value != 0:
             w.value = 0

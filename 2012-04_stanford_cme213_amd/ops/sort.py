@@ -2,7 +2,13 @@
 merge-path merge sort, and the hw4 OpenMP radix / merge sorts.
 
 Keys: uint32 natively; int32 and float32 are mapped to order-preserving
-uint32 codes (sign-bit flip / IEEE total-order trick) and back.
+uint32 codes (sign-bit flip / IEEE total-order trick) and back -- inside the
+onesweep kernels (first pass loads, last pass stores), elsewhere by tensor ops.
+
+GPU radix algorithms: "radix" = onesweep (``csrc/hip/radix.hip``: one
+histogram read for every pass, then one read + one write of the keys per
+8-bit digit with decoupled look-back), "radix_rts" = the reduce-then-scan
+form (``csrc/hip/sort.hip``: upsweep + scan + downsweep per digit).
 """
 from __future__ import annotations
 
@@ -11,7 +17,9 @@ import torch
 from .. import _ext
 
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_sort_u32", "ppppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_radix_onesweep", "ppppppqiiipqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
+_ext.proto(_ext.HIP_PROTOS, "cme_merge_sort", "ppppppqip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_u32", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_serial_u32", "ppqi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_merge_sort_i32", "ppqqqp")
@@ -43,6 +51,86 @@ def _from_u32(u: torch.Tensor, dtype) -> torch.Tensor:
 
 
 _ws: dict = {}
+_os_ws: dict = {}
+_os_epochs: dict = {}
+_OS_TILE = 8192
+_OS_EPOCH_LIMIT = 1 << 27  # radix.hip: granule tag = epoch * 4 + pass, 30 bits
+_MODES = {torch.uint32: 0, torch.int32: 1, torch.float32: 2}
+
+
+def _onesweep_ws(keys: torch.Tensor) -> tuple[torch.Tensor, int]:
+    """Workspace + call epoch of a onesweep sort (cf. ops/scan.py
+    _lookback_ws): zeroed once when (re)allocated, then every call gets the
+    next epoch, so granules of earlier calls never match and no memset runs.
+    Keyed by (device, stream); under stream capture a separate workspace with
+    epoch 0, which the launcher zeroes inside the graph at every replay."""
+    n = keys.numel()
+    tiles = (n + _OS_TILE - 1) // _OS_TILE
+    nbytes = 2 * 4 * 256 * 4 + tiles * 8 + tiles * 256 * 8 + 256  # = cme_radix_onesweep_ws_bytes
+    capturing = torch.cuda.is_current_stream_capturing()
+    k = (f"os:{'cap:' if capturing else ''}{_ext.stream_ptr(keys.device)}", keys.device.index)
+    t = _os_ws.get(k)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=keys.device)
+        _os_ws[k] = t
+        _os_epochs[k] = 0
+    if capturing:
+        return t, 0
+    e = _os_epochs[k] + 1
+    if e >= _OS_EPOCH_LIMIT:
+        t.zero_()
+        e = 1
+    _os_epochs[k] = e
+    return t, e
+
+
+def _merge(keys: torch.Tensor, values: torch.Tensor | None):
+    """GPU merge sort (csrc/hip/sort.hip cme_merge_sort): stable; 4096-key
+    block sorts, then one LDS-staged merge-path pass per doubling of the run
+    length; key transforms fused into the first and last kernels."""
+    if keys.dtype not in _MODES:
+        raise TypeError(f"unsupported key dtype {keys.dtype}")
+    k = keys.contiguous()
+    out, tmp = torch.empty_like(k), torch.empty_like(k)
+    vp = vo = vt = None
+    if values is not None:
+        if values.element_size() != 4 or values.numel() != k.numel():
+            raise TypeError("values: one 32-bit value per key")
+        v = values.contiguous()
+        vout, vtmp = torch.empty_like(v), torch.empty_like(v)
+        vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
+    _ext.call_hip("cme_merge_sort", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
+                  _MODES[keys.dtype], _ext.stream_ptr(keys.device))
+    return (out, vout) if values is not None else out
+
+
+def _onesweep(keys: torch.Tensor, values: torch.Tensor | None, key_bits: int):
+    from .scan import _check_lookback
+
+    n = keys.numel()
+    dtype = keys.dtype
+    if dtype not in _MODES:
+        raise TypeError(f"unsupported key dtype {dtype}")
+    if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
+        raise TypeError("key_bits < 32 needs non-negative integer keys")
+    mode = 0 if key_bits < 32 else _MODES[dtype]
+    bits = 32 if key_bits >= 32 else max(1, int(key_bits))
+    k = keys.contiguous()
+    out = torch.empty_like(k)
+    tmp = torch.empty_like(k)
+    vp = vo = vt = None
+    if values is not None:
+        if values.element_size() != 4 or values.numel() != n:
+            raise TypeError("values: one 32-bit value per key")
+        v = values.contiguous()
+        vout, vtmp = torch.empty_like(v), torch.empty_like(v)
+        vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
+    ws, epoch = _onesweep_ws(k)
+    _check_lookback(k, before=True)
+    _ext.call_hip("cme_radix_onesweep", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, n, mode, 0, bits,
+                  ws.data_ptr(), epoch, _ext.stream_ptr(keys.device))
+    _check_lookback(k)
+    return (out, vout) if values is not None else out
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
@@ -56,7 +144,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "radix", num_bits: int = 8,
          key_bits: int = 32):
     """Sort a 1-D tensor (optionally carrying int32/uint32/float32 values).
-    GPU algos: "radix" (stable), "merge". CPU algos: "radix" (OpenMP,
+    GPU algos: "radix" (onesweep, stable), "radix_rts" (reduce-then-scan,
+    stable), "merge". CPU algos: "radix" (OpenMP,
     ``num_bits`` per pass), "radix_serial", "merge" (OpenMP tasks, keys only).
     ``key_bits`` < 32 (GPU radix, non-negative integer keys below
     ``2**key_bits``) runs only the passes covering those bits -- a counting
@@ -65,6 +154,12 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
         raise ValueError("1-D keys expected")
     n = keys.numel()
     dtype = keys.dtype
+    if keys.is_cuda and algo == "radix":
+        if n <= 1:
+            return (keys.clone(), values.clone()) if values is not None else keys.clone()
+        return _onesweep(keys, values, key_bits)
+    if keys.is_cuda and algo == "merge":
+        return _merge(keys, values)
     if keys.is_cuda:
         k = _to_u32(keys.contiguous())
         k2 = torch.empty_like(k)
@@ -75,7 +170,7 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
         s = _ext.stream_ptr(keys.device)
         vp = v.data_ptr() if v is not None else None
         v2p = v2.data_ptr() if v2 is not None else None
-        if algo == "radix":
+        if algo == "radix_rts":
             ws = _workspace(keys.device, 2 * 1024 * 256 * 4 + 65536)
             if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
                 raise TypeError("key_bits < 32 needs non-negative integer keys")
@@ -87,8 +182,6 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
             if key_bits < 32 and dtype == torch.int32:
                 out = k.view(torch.int32)
                 return (out, v.view(values.dtype)) if values is not None else out
-        elif algo == "merge":
-            _ext.call_hip("cme_merge_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, s)
         else:
             raise ValueError(algo)
         out = _from_u32(k, dtype)

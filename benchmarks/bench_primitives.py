@@ -156,6 +156,14 @@ def main():
             ms = timeit(lambda: iterate(g, x0, 20, grp))
             emit(bench="pagerank", group=grp, ms=ms, GBps_model=bytes_model(g, 20) / ms / 1e6, ref_ms=1188.11,
                  speedup_vs_ref=1188.11 / ms)
+        from cme213x.ops.graph import block_columns
+
+        for blocks in (2, 4, 8):
+            bg = block_columns(g, blocks)
+            for grp in (1, 2, 4):
+                ms = timeit(lambda: iterate(bg, x0, 20, grp))
+                emit(bench="pagerank", blocks=blocks, group=grp, ms=ms, GBps_model=bytes_model(g, 20) / ms / 1e6,
+                     ref_ms=1188.11, speedup_vs_ref=1188.11 / ms)
 
 
 def bench_transpose(emit, timeit):

@@ -365,7 +365,11 @@ CME_EXPORT int cme_sgemm_tune(int M, int N, int K, const float* A, const float* 
 CME_EXPORT int cme_sgemm(int M, int N, int K, float alpha, const float* A, const float* B, float beta, float* C,
                          int variant, void* stream) {
     hipStream_t s = as_stream(stream);
-    if (variant == 2 && (M % MT || N % MT || K % MK || ((uintptr_t)A % 16) || ((uintptr_t)B % 16))) variant = 1;
+    // the MFMA epilogue stores (and, with beta != 0, loads) 16-B vectors of C: an
+    // offset view of C that is not 16-B aligned takes the LDS kernel too
+    if (variant == 2 && (M % MT || N % MT || K % MK || ((uintptr_t)A % 16) || ((uintptr_t)B % 16) ||
+                         ((uintptr_t)C % 16)))
+        variant = 1;
     switch (variant) {
         case 0:
             hipLaunchKernelGGL(sgemm_naive_kernel, dim3(cdiv(N, 64), cdiv(M, 4)), dim3(256), 0, s, M, N, K, alpha, A,

@@ -98,7 +98,76 @@ __global__ __launch_bounds__(256) void pr_group_kernel(const uint32_t* __restric
     }
 }
 
+// Column-blocked sweep (one launch per source block b of B): the edges are
+// pre-sorted by (block of the gathered node, row), so a launch gathers only
+// from y[b*bs, (b+1)*bs) -- 2 MB for 2^21 nodes and B = 4, resident in every
+// XCD's 4 MB L2 while the edge stream passes through -- instead of the whole
+// 8 MB vector (half of each gather line missing L2 into the Infinity Cache).
+// Per row the block sums are accumulated in `acc` in block order; the last
+// block applies 0.5/N + 0.5*sum and emits out and the next sweep's y.
+template <int G>
+__global__ __launch_bounds__(256) void pr_blocked_kernel(const uint32_t* __restrict__ rp,
+                                                         const uint32_t* __restrict__ edges,
+                                                         const float* __restrict__ y_in, float* __restrict__ acc,
+                                                         float* __restrict__ out, float* __restrict__ y_out,
+                                                         const float* __restrict__ inv, int n, int first, int last) {
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    const int sub = threadIdx.x % G;
+    float sum = 0.f;
+    if (gid < n) {
+        const uint32_t b = rp[gid], e = rp[gid + 1];
+        for (uint32_t j = b + sub; j < e; j += G) sum += y_in[__builtin_nontemporal_load(edges + j)];
+    }
+    if constexpr (G >= 2) sum += __shfl_xor(sum, 1, 64);
+    if constexpr (G >= 4) sum += __shfl_xor(sum, 2, 64);
+    if constexpr (G >= 8) sum += __shfl_xor(sum, 4, 64);
+    if (gid < n && sub == 0) {
+        const float a = first ? sum : acc[gid] + sum;
+        if (last) {
+            const float o = 0.5f / (float)n + 0.5f * a;
+            out[gid] = o;
+            y_out[gid] = o * inv[gid];
+        } else {
+            acc[gid] = a;
+        }
+    }
+}
+
 }  // namespace
+
+// One blocked sweep: `blocks` launches over the (block, row)-sorted edges;
+// rp holds blocks*n + 1 offsets (row i of block b: [rp[b*n+i], rp[b*n+i+1])).
+CME_EXPORT int cme_pr_propagate_blocked(const uint32_t* rp, const uint32_t* edges, const float* y_in, float* acc,
+                                        float* out, float* y_out, const float* inv, int n, int blocks, int group,
+                                        void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (blocks < 1) return (int)hipErrorInvalidValue;
+    for (int b = 0; b < blocks; ++b) {
+        const uint32_t* r = rp + (size_t)b * n;
+        const int first = b == 0, last = b == blocks - 1;
+        switch (group) {
+            case 1:
+                hipLaunchKernelGGL(pr_blocked_kernel<1>, dim3(cdiv(n, 256)), dim3(256), 0, s, r, edges, y_in, acc, out,
+                                   y_out, inv, n, first, last);
+                break;
+            case 2:
+                hipLaunchKernelGGL(pr_blocked_kernel<2>, dim3(cdiv((size_t)n * 2, 256)), dim3(256), 0, s, r, edges,
+                                   y_in, acc, out, y_out, inv, n, first, last);
+                break;
+            case 4:
+                hipLaunchKernelGGL(pr_blocked_kernel<4>, dim3(cdiv((size_t)n * 4, 256)), dim3(256), 0, s, r, edges,
+                                   y_in, acc, out, y_out, inv, n, first, last);
+                break;
+            case 8:
+                hipLaunchKernelGGL(pr_blocked_kernel<8>, dim3(cdiv((size_t)n * 8, 256)), dim3(256), 0, s, r, edges,
+                                   y_in, acc, out, y_out, inv, n, first, last);
+                break;
+            default: return (int)hipErrorInvalidValue;
+        }
+        CME_TRY(hipGetLastError());
+    }
+    return 0;
+}
 
 CME_EXPORT int cme_pr_prescale(const float* x, const float* inv, float* y, int n, void* stream) {
     hipLaunchKernelGGL(prescale_kernel, dim3(cdiv(n, 256)), dim3(256), 0, as_stream(stream), x, inv, y, n);
@@ -144,3 +213,4 @@ CME_EXPORT int cme_pr_propagate(const uint32_t* idx, const uint32_t* edges, cons
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(pagerank_ref, 256, pr_ref_kernel);
 CME_REGISTER_KERNEL(pagerank_group8, 256, pr_group_kernel<8>);
+CME_REGISTER_KERNEL(pagerank_blocked2, 256, pr_blocked_kernel<2>);

@@ -22,17 +22,23 @@ using namespace cme;
 
 // The look-back give-up word: pinned, mapped host memory (lookback.h). One per
 // process; device stores reach it directly, the host reads it without a sync.
+// One give-up word per device (its own 64-B line): a timed-out launch on one
+// GPU does not poison look-back launches on another.
 unsigned* cme::lb_host_timeout() {
-    static unsigned* w = [] {
+    static unsigned* words = [] {
         void* p = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return (unsigned*)nullptr;
-        *(volatile unsigned*)p = 0u;
+        if (hipHostMalloc(&p, 64 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return (unsigned*)nullptr;
+        for (int i = 0; i < 64 * 16; ++i) ((volatile unsigned*)p)[i] = 0u;
         return (unsigned*)p;
     }();
-    return w;
+    if (!words) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return words + 16 * (dev & 63);
 }
 
-// Host address of that word (ops/scan.py reads / clears it).
+// Host address of the current device's word (ops/scan.py reads / clears it).
 CME_EXPORT int cme_lookback_timeout_word(void** host_word) {
     unsigned* w = lb_host_timeout();
     if (!w) return (int)hipErrorOutOfMemory;

@@ -163,88 +163,223 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
 }
 
 // ------------------------------------------------------------ merge sort
-// Block-local bitonic sort of 1024-key tiles (4 keys per thread) in LDS.
-constexpr int kMsTile = 1024;
+// Stable merge sort in two kernels (wave64, LDS-staged; the hw4 merge sort's
+// median split + upper_bound merge, hw/hw4/programming/mergesort.cpp:31-144,
+// becomes a merge-path split):
+//   block sort : a 256-lane block sorts a 4096-key tile: 16 consecutive keys
+//                per lane sorted in registers by odd-even transposition
+//                (stable), then 8 rounds of merge path in LDS (runs of 16 ->
+//                4096, A first on ties: stable);
+//   merge pass : output tile o (4096 keys) of a pass merging runs of L: the
+//                block finds its two diagonal splits by a cooperative 128-ary
+//                search (2 x 128 lanes, ~4 dependent rounds of global loads
+//                instead of ~24), loads the A and B pieces into LDS with
+//                coalesced loads, merges 16 outputs per lane from LDS and
+//                stores the tile coalesced through LDS.
+// Keys are uint32 codes (int32 / float32 mapped on the block sort's loads and
+// back on the last pass's stores, as the radix sort does). Values optional.
+constexpr int kMsThreads = 256;
+constexpr int kMsItems = 16;
+constexpr int kMsTile = kMsThreads * kMsItems;  // 4096
 
-template <bool HAS_VALUES>
-__global__ __launch_bounds__(256) void bitonic_tile_kernel(uint32_t* keys, uint32_t* vals, long long n) {
-    __shared__ uint32_t sk[kMsTile];
-    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
-    const long long base = (long long)blockIdx.x * kMsTile;
-    for (int i = threadIdx.x; i < kMsTile; i += 256) {
-        const bool ok = base + i < n;
-        sk[i] = ok ? keys[base + i] : 0xffffffffu;
-        if constexpr (HAS_VALUES) sv[i] = ok ? vals[base + i] : 0u;
-    }
-    __syncthreads();
-    for (int size = 2; size <= kMsTile; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < kMsTile / 2; t += 256) {
-                const int i = 2 * t - (t & (stride - 1));
-                const int j = i + stride;
-                const bool up = ((i & size) == 0);
-                const uint32_t a = sk[i], b = sk[j];
-                // stable tie-break is impossible in bitonic; ties keep order
-                // within a key only for keys (values of equal keys may swap)
-                if ((a > b) == up) {
-                    sk[i] = b;
-                    sk[j] = a;
-                    if constexpr (HAS_VALUES) {
-                        const uint32_t x = sv[i];
-                        sv[i] = sv[j];
-                        sv[j] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = threadIdx.x; i < kMsTile; i += 256)
-        if (base + i < n) {
-            keys[base + i] = sk[i];
-            if constexpr (HAS_VALUES) vals[base + i] = sv[i];
-        }
+__device__ __forceinline__ uint32_t ms_key_in(uint32_t k, int mode) {
+    if (mode == 1) return k ^ 0x80000000u;
+    if (mode == 2) return k ^ ((uint32_t)((int)k >> 31) | 0x80000000u);
+    return k;
+}
+__device__ __forceinline__ uint32_t ms_key_out(uint32_t u, int mode) {
+    if (mode == 1) return u ^ 0x80000000u;
+    if (mode == 2) return u ^ (((uint32_t)((int)u >> 31) ^ 0xffffffffu) | 0x80000000u);
+    return u;
 }
 
-// Merge path: merge pairs of sorted runs of length `run` from src into dst.
-// Each lane produces kMP consecutive outputs: it finds its diagonal split by
-// binary search (upper/lower bound, A-first on ties: stable) then merges.
-constexpr int kMP = 8;
-
-template <bool HAS_VALUES>
-__global__ __launch_bounds__(256) void merge_pass_kernel(const uint32_t* __restrict__ sk, uint32_t* __restrict__ dk,
-                                                         const uint32_t* __restrict__ sv, uint32_t* __restrict__ dv,
-                                                         long long n, long long run) {
-    const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    const long long out0 = tid * kMP;
-    if (out0 >= n) return;
-    const long long pair = out0 / (2 * run);
-    const long long a0 = pair * 2 * run;
-    const long long a1 = a0 + run < n ? a0 + run : n;
-    const long long b1 = a1 + run < n ? a1 + run : n;
-    const long long la = a1 - a0, lb = b1 - a1;
-    const long long diag = out0 - a0;
-    // find i in [max(0, diag-lb), min(diag, la)] with A[i-1] <= B[diag-i] and B[diag-i-1] < A[i]
-    long long lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
+// merge-path split of diagonal `diag` between A[0, la) and B[0, lb) (LDS or
+// registers-free generic accessor): number of A elements among the first
+// `diag` outputs, A first on ties
+template <typename FA, typename FB>
+__device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
+    int lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
     while (lo < hi) {
-        const long long mid = (lo + hi) >> 1;
-        if (sk[a0 + mid] <= sk[a1 + diag - mid - 1]) lo = mid + 1;
+        const int mid = (lo + hi) >> 1;
+        if (A(mid) <= B(diag - 1 - mid)) lo = mid + 1;
         else hi = mid;
     }
-    long long i = lo, j = diag - lo;
-    const long long end = out0 + kMP < b1 ? out0 + kMP : b1;
-    for (long long o = out0; o < end; ++o) {
-        const bool take_a = (i < la) && (j >= lb || sk[a0 + i] <= sk[a1 + j]);
+    return lo;
+}
+
+// sequential merge of `cnt` outputs from A[i..la) / B[j..lb) (LDS) into registers
+template <bool HAS_VALUES>
+__device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* sv, int a0, int la, int b0, int lb,
+                                           int i, int j, uint32_t (&k)[kMsItems], uint32_t (&v)[kMsItems]) {
+    uint32_t ka = i < la ? sk[a0 + i] : 0xffffffffu, kb = j < lb ? sk[b0 + j] : 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < kMsItems; ++q) {
+        const bool take_a = j >= lb || (i < la && ka <= kb);
+        k[q] = take_a ? ka : kb;
+        if constexpr (HAS_VALUES) {
+            const int x = take_a ? a0 + i : b0 + j;  // past both ends only on padding lanes
+            v[q] = sv[x < kMsTile ? x : kMsTile - 1];
+        }
         if (take_a) {
-            dk[o] = sk[a0 + i];
-            if constexpr (HAS_VALUES) dv[o] = sv[a0 + i];
             ++i;
+            ka = i < la ? sk[a0 + i] : 0xffffffffu;
         } else {
-            dk[o] = sk[a1 + j];
-            if constexpr (HAS_VALUES) dv[o] = sv[a1 + j];
             ++j;
+            kb = j < lb ? sk[b0 + j] : 0xffffffffu;
         }
     }
+}
+
+// coalesced tile store through LDS: lane t holds outputs [16t, 16t+16)
+template <bool HAS_VALUES>
+__device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const uint32_t (&k)[kMsItems],
+                                              const uint32_t (&v)[kMsItems], uint32_t* __restrict__ ko,
+                                              uint32_t* __restrict__ vo, long long base, int cnt, int mode) {
+    __syncthreads();  // every lane is done reading the tile in LDS
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kMsItems; ++q) {
+        sk[kMsItems * t + q] = k[q];
+        if constexpr (HAS_VALUES) sv[kMsItems * t + q] = v[q];
+    }
+    __syncthreads();
+    for (int i = t; i < cnt; i += kMsThreads) {
+        ko[base + i] = ms_key_out(sk[i], mode);
+        if constexpr (HAS_VALUES) vo[base + i] = sv[i];
+    }
+}
+
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(kMsThreads) void ms_block_sort_kernel(const uint32_t* __restrict__ ki,
+                                                                   uint32_t* __restrict__ ko,
+                                                                   const uint32_t* __restrict__ vi,
+                                                                   uint32_t* __restrict__ vo, long long n,
+                                                                   int mode_in, int mode_out) {
+    __shared__ uint32_t sk[kMsTile];
+    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
+    const int t = threadIdx.x;
+    const long long base = (long long)blockIdx.x * kMsTile;
+    const int cnt = (int)(n - base < kMsTile ? n - base : kMsTile);
+    // coalesced load into LDS, then lane t takes keys [16t, 16t+16)
+    for (int i = t; i < kMsTile; i += kMsThreads) {
+        sk[i] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
+        if constexpr (HAS_VALUES) sv[i] = i < cnt ? vi[base + i] : 0u;
+    }
+    __syncthreads();
+    uint32_t k[kMsItems], v[kMsItems];
+#pragma unroll
+    for (int q = 0; q < kMsItems; ++q) {
+        k[q] = sk[kMsItems * t + q];
+        if constexpr (HAS_VALUES) v[q] = sv[kMsItems * t + q];
+    }
+    // odd-even transposition: swaps only strictly greater neighbours (stable);
+    // padding keys (all ones) sit at the tile's end and stay behind real keys
+#pragma unroll
+    for (int r = 0; r < kMsItems; ++r) {
+#pragma unroll
+        for (int q = r & 1; q + 1 < kMsItems; q += 2) {
+            if (k[q] > k[q + 1]) {
+                const uint32_t x = k[q];
+                k[q] = k[q + 1];
+                k[q + 1] = x;
+                if constexpr (HAS_VALUES) {
+                    const uint32_t y = v[q];
+                    v[q] = v[q + 1];
+                    v[q + 1] = y;
+                }
+            }
+        }
+    }
+    // merge rounds in LDS: runs of 16 << r
+    for (int L = kMsItems; L < kMsTile; L <<= 1) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kMsItems; ++q) {
+            sk[kMsItems * t + q] = k[q];
+            if constexpr (HAS_VALUES) sv[kMsItems * t + q] = v[q];
+        }
+        __syncthreads();
+        const int out0 = kMsItems * t;
+        const int a0 = out0 & ~(2 * L - 1), b0 = a0 + L;
+        const int diag = out0 - a0;
+        const int i = ms_split([&](int x) { return sk[a0 + x]; }, [&](int x) { return sk[b0 + x]; }, L, L, diag);
+        ms_merge16<HAS_VALUES>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
+    }
+    ms_store_tile<HAS_VALUES>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
+}
+
+// Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
+// 2*part+1) narrow [lo, hi] 128-fold per round, one global load pair per
+// lane, for a fixed `rounds` (uniform across the block: both parts pass the
+// same barriers). Q(m) = A[m] <= B[diag-1-m] holds below the answer (A first
+// on ties) and fails from it on; returns the answer.
+__device__ __forceinline__ long long ms_coop_split(const uint32_t* __restrict__ A, const uint32_t* __restrict__ B,
+                                                   long long la, long long lb, long long diag, int rounds,
+                                                   uint64_t (*smask)[2]) {
+    const int t = threadIdx.x, part = t >> 7, l = t & 127, w = (t >> 6) & 1;
+    long long lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
+    for (int r = 0; r < rounds; ++r) {
+        const long long step = (hi - lo + 127) / 128;
+        const long long m = lo + (long long)l * step;
+        const bool q = lo < hi && m < hi && A[m] <= B[diag - 1 - m];
+        const uint64_t fails = __ballot(!q);
+        if ((t & 63) == 0) smask[part][w] = fails;
+        __syncthreads();
+        const uint64_t f0 = smask[part][0], f1 = smask[part][1];
+        const int f = f0 ? __builtin_ctzll(f0) : (f1 ? 64 + __builtin_ctzll(f1) : 128);
+        __syncthreads();
+        if (lo < hi) {
+            const long long nlo = f == 0 ? lo : lo + (long long)(f - 1) * step + 1;
+            const long long mf = lo + (long long)f * step;
+            const long long nhi = f == 128 ? hi : (mf < hi ? mf : hi);
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    return lo;
+}
+
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_t* __restrict__ ki,
+                                                                   uint32_t* __restrict__ ko,
+                                                                   const uint32_t* __restrict__ vi,
+                                                                   uint32_t* __restrict__ vo, long long n,
+                                                                   long long L, int mode_out) {
+    __shared__ uint32_t sk[kMsTile];
+    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
+    __shared__ uint64_t smask[2][2];
+    __shared__ long long ssplit[2];
+    const int t = threadIdx.x;
+    const long long o0 = (long long)blockIdx.x * kMsTile;
+    const long long o1 = o0 + kMsTile < n ? o0 + kMsTile : n;
+    const long long a0 = o0 & ~(2 * L - 1);  // pair start (2L is a multiple of the tile)
+    const long long la = a0 + L < n ? L : n - a0;
+    const long long lb = a0 + 2 * L < n ? L : (n - a0 - la > 0 ? n - a0 - la : 0);
+    const uint32_t* A = ki + a0;
+    const uint32_t* B = ki + a0 + la;
+    const int part = t >> 7;
+    const long long diag = (part == 0 ? o0 : o1) - a0;
+    int rounds = 0;  // ceil(log_128(L + 1)): candidates per search <= L + 1
+    for (long long w = L + 1; w > 1; w = (w + 127) / 128) ++rounds;
+    const long long sp = ms_coop_split(A, B, la, lb, diag, rounds, smask);
+    if ((t & 127) == 0) ssplit[part] = sp;
+    __syncthreads();
+    const long long i0 = ssplit[0], i1 = ssplit[1];
+    const long long j0 = (o0 - a0) - i0, j1 = (o1 - a0) - i1;
+    const int na = (int)(i1 - i0), nb = (int)(j1 - j0);
+    for (int x = t; x < na + nb; x += kMsThreads) {
+        const bool ia = x < na;
+        const long long g = ia ? a0 + i0 + x : a0 + la + j0 + (x - na);
+        sk[x] = ki[g];
+        if constexpr (HAS_VALUES) sv[x] = vi[g];
+    }
+    __syncthreads();
+    const int cnt = na + nb;
+    const int diag_l = kMsItems * t < cnt ? kMsItems * t : cnt;
+    const int i = ms_split([&](int x) { return sk[x]; }, [&](int x) { return sk[na + x]; }, na, nb, diag_l);
+    uint32_t k[kMsItems], v[kMsItems];
+    ms_merge16<HAS_VALUES>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
+    ms_store_tile<HAS_VALUES>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
 }
 
 }  // namespace
@@ -300,38 +435,55 @@ CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
     CME_LAUNCH_STATUS();
 }
 
-// Merge sort: bitonic 1024-key tiles, then merge-path passes. Result in keys.
+// Stable merge sort of n keys from `in` into `out` (ping-pong through `tmp`;
+// `in` may equal `out`; values optional, likewise). mode: 0 uint32, 1 int32,
+// 2 float32 keys.
+CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
+                              uint32_t* vtmp, long long n, int mode, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 0) return 0;
+    if (mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) || (vin && !vtmp))
+        return (int)hipErrorInvalidValue;
+    int npass = 0;
+    for (long long L = kMsTile; L < n; L <<= 1) ++npass;
+    // the block sort writes where an even number of passes later lands in out
+    uint32_t* d0 = (npass & 1) ? tmp : out;
+    uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
+    const unsigned tiles = cdiv(n, kMsTile);
+    if (vin)
+        hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, in, d0, vin, v0, n, mode,
+                           npass ? 0 : mode);
+    else
+        hipLaunchKernelGGL(ms_block_sort_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, in, d0, vin, v0, n, mode,
+                           npass ? 0 : mode);
+    CME_TRY(hipGetLastError());
+    const uint32_t *ki = d0, *vi = v0;
+    int p = 0;
+    for (long long L = kMsTile; L < n; L <<= 1, ++p) {
+        const bool last = p == npass - 1;
+        uint32_t* ko = (ki == out) ? tmp : out;
+        uint32_t* vo = vin ? ((vi == vout) ? vtmp : vout) : nullptr;
+        if (vin)
+            hipLaunchKernelGGL(ms_merge_pass_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n, L,
+                               last ? mode : 0);
+        else
+            hipLaunchKernelGGL(ms_merge_pass_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n,
+                               L, last ? mode : 0);
+        CME_TRY(hipGetLastError());
+        ki = ko;
+        vi = vo;
+    }
+    return 0;
+}
+
+// In-place form (keys sorted into `keys`; keys_alt / vals_alt scratch).
 CME_EXPORT int cme_merge_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, long long n,
                                   void* stream) {
-    hipStream_t s = as_stream(stream);
-    if (n <= 1) return 0;
-    const unsigned tiles = cdiv(n, kMsTile);
-    if (vals) hipLaunchKernelGGL(bitonic_tile_kernel<true>, dim3(tiles), dim3(256), 0, s, keys, vals, n);
-    else hipLaunchKernelGGL(bitonic_tile_kernel<false>, dim3(tiles), dim3(256), 0, s, keys, vals, n);
-    CME_TRY(hipGetLastError());
-    uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
-    int passes = 0;
-    for (long long run = kMsTile; run < n; run <<= 1, ++passes) {
-        const unsigned grid = cdiv(cdiv(n, kMP), 256);
-        if (vals) hipLaunchKernelGGL(merge_pass_kernel<true>, dim3(grid), dim3(256), 0, s, ki, ko, vi, vo, n, run);
-        else hipLaunchKernelGGL(merge_pass_kernel<false>, dim3(grid), dim3(256), 0, s, ki, ko, vi, vo, n, run);
-        CME_TRY(hipGetLastError());
-        uint32_t* t = ki;
-        ki = ko;
-        ko = t;
-        t = vi;
-        vi = vo;
-        vo = t;
-    }
-    if (passes & 1) {
-        CME_TRY(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToDevice, s));
-        if (vals) CME_TRY(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToDevice, s));
-    }
-    CME_LAUNCH_STATUS();
+    return cme_merge_sort(keys, keys, keys_alt, vals, vals, vals_alt, n, 0, stream);
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel);
 CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
-CME_REGISTER_KERNEL(bitonic_tile, 256, bitonic_tile_kernel<false>);
-CME_REGISTER_KERNEL(merge_pass, 256, merge_pass_kernel<false>);
+CME_REGISTER_KERNEL(ms_block_sort, 256, ms_block_sort_kernel<false>);
+CME_REGISTER_KERNEL(ms_merge_pass, 256, ms_merge_pass_kernel<false>);

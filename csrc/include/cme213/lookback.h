@@ -26,11 +26,11 @@ namespace cme {
 // when its epoch matches, so a multi-iteration driver zeroes the array ONCE
 // and gives iteration i epoch i+1 (epoch 0 never matches a zeroed word).
 enum : uint32_t { kStInvalid = 0, kStAggregate = 1, kStInclusive = 2, kStFlag = 4 };
-// Bounded spins: ~2^18 polls (well under a second) per wait, and the timeout
+// Bounded spins: ~2^20 polls (about a second) per wait, and the timeout
 // word is STICKY -- every 256 polls a waiter re-reads it and gives up at once
 // if any tile already timed out, so a broken launch (e.g. a grid that is not
 // co-resident) ends in about one spin limit instead of one per tile.
-constexpr unsigned kSpinLimit = 1u << 18;
+constexpr unsigned kSpinLimit = 1u << 20;
 
 __device__ __forceinline__ bool lb_give_up(unsigned spins, unsigned* timeout, int lane) {
     if (spins > kSpinLimit) {
@@ -42,11 +42,11 @@ __device__ __forceinline__ bool lb_give_up(unsigned spins, unsigned* timeout, in
     return false;
 }
 
-// The timeout word the kernels set lives in pinned, mapped HOST memory
-// (lb_host_timeout, scan.hip): it is never reset by a launch, so a timed-out
-// launch poisons the following ones (they give up at once) until the host
-// reads and clears it -- ops/scan.py does that before every look-back call
-// and raises, without a device synchronisation.
+// The timeout word the kernels set lives in pinned, mapped HOST memory, one
+// per device (lb_host_timeout, scan.hip): it is never reset by a launch, so a
+// timed-out launch poisons the following ones on that device (they give up
+// at once) until the host reads and clears it -- ops/scan.py does that
+// before every look-back call and raises, without a device synchronisation.
 unsigned* lb_host_timeout();
 
 // Workspace layout: [0, 16) unused pad, [16, 16 + 8*tiles) descriptors.

@@ -63,3 +63,18 @@ def test_gemv_gpu(gpu, dtype, shape):
     Au = buf[1:].view(M, K)
     out2 = gemv(Au, x.to(gpu)).cpu()
     torch.testing.assert_close(out2.double(), Au.cpu().double() @ x.double(), rtol=tol, atol=tol * max(1.0, K ** 0.5))
+
+
+@pytest.mark.gpu
+def test_sgemm_mfma_misaligned_c_view(gpu):
+    """the MFMA epilogue stores 16-B vectors of C; an offset view of
+    C (4-B aligned only) must take the fallback, not misaligned vector stores."""
+    M = N = 256
+    K = 64
+    A, B = torch.randn(M, K), torch.randn(K, N)
+    big = torch.randn(M * N + 1)
+    Cv = big[1:].view(M, N)
+    ref = (A.double().mm(B.double()) + 0.5 * Cv.double()).float()
+    Cg = big.to(gpu)[1:].view(M, N)
+    out = sgemm(A.to(gpu), B.to(gpu), Cg, 1.0, 0.5, variant="mfma").cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3)
