@@ -66,7 +66,7 @@ def _onesweep_ws(keys: torch.Tensor) -> tuple[torch.Tensor, int]:
     epoch 0, which the launcher zeroes inside the graph at every replay."""
     n = keys.numel()
     tiles = (n + _OS_TILE - 1) // _OS_TILE
-    nbytes = 2 * 4 * 256 * 4 + tiles * 8 + tiles * 256 * 8 + 256  # = cme_radix_onesweep_ws_bytes
+    nbytes = 2 * 4 * 256 * 4 + tiles * 8 + 2 * tiles * 256 * 8 + 256  # = cme_radix_onesweep_ws_bytes
     capturing = torch.cuda.is_current_stream_capturing()
     k = (f"os:{'cap:' if capturing else ''}{_ext.stream_ptr(keys.device)}", keys.device.index)
     t = _os_ws.get(k)

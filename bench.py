@@ -217,7 +217,11 @@ def main() -> int:
 
                     native = NativeRccl()
                 if args.native == "auto":
-                    native_ok = selftest(comm, native, dev, args, fused=fused)
+                    try:
+                        native_ok = selftest(comm, native, dev, args, fused=fused)
+                    except Exception as e:  # noqa: BLE001 - e.g. the fused launch refused its gated grid
+                        print(f"bench.py rank {rank}: native self-test raised ({e})", file=sys.stderr)
+                        native_ok = False
                     if not agree(native_ok) and fused:
                         # the fused gated schedule failed (or its probe refused
                         # it on some rank): retry the native loop on schedule 0

@@ -836,13 +836,15 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if (nsub < 1 || nsub > kMaxSubs) return (int)hipErrorInvalidValue;
     if ((transport == 0 || transport == 3) && nsub != 1) return (int)hipErrorInvalidValue;
     if (transport < 0 || transport > 3) return (int)hipErrorInvalidValue;
+    // Stream capture is refused: the fused schedule's gate target
+    // and the IPC epochs are host counters baked into kernel arguments, so a
+    // replay would see stale flags as already reached; and instantiating a
+    // capture of the multi-stream event schedule crashes this image's HIP
+    // runtime in capture_end (profiles/dist_rank_r2.md). The loop is issued
+    // from C++ with no host synchronisation, so there is little to gain.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     CME_TRY(hipStreamIsCapturing(s, &cap));
-    const bool capturing = cap != hipStreamCaptureStatusNone;
-    // IPC epochs are host counters baked into the wait / signal kernels: a
-    // captured IPC run would replay stale epochs (peers' staging read before
-    // it is packed) -- refused
-    if (capturing && transport == 3) return (int)hipErrorStreamCaptureUnsupported;
+    if (cap != hipStreamCaptureStatusNone) return (int)hipErrorStreamCaptureUnsupported;
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
     if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4 && !(fma & kKernelPipe)))
         return (int)hipErrorInvalidValue;
@@ -861,12 +863,9 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     // pass at N = 8, profiles/dist_fused_r2.md). Pipelined passes (fp32 or
     // fp64), one subdomain per process, and only when
     //  * the caller did not ask for schedule 0 (kNoFused bit of `fma`),
-    //  * the caller's stream is not being captured into a graph (the gate
-    //    target and the flag are host-side counters baked into the kernel
-    //    arguments: a replay would see stale flags as already reached),
     //  * the queue-independence probe passed (run_gate_probe).
     // Other configurations use schedule 0.
-    bool fused = schedule == 2 && !(fma & kNoFused) && !capturing && !sync && nsub == 1 && (fma & kKernelPipe) &&
+    bool fused = schedule == 2 && !(fma & kNoFused) && !sync && nsub == 1 && (fma & kKernelPipe) &&
                  tblock >= 3 && transport != 1 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions &&
                  subs[0].n_int >= 1;
     DistCtx* ctx;
@@ -941,9 +940,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     }
     // Events recorded by THIS call. Everything an earlier call queued is
     // already ordered before ev_start (the caller's stream joined all of it),
-    // so waits on events of earlier calls are skipped: redundant in eager
-    // mode, and not allowed while the caller's stream is being captured into
-    // a hipGraph (a graph may only depend on work captured with it).
+    // so waits on events of earlier calls are skipped as redundant.
     bool comm_rec = false, int_rec[2] = {false, false}, border_rec[2] = {false, false};
     auto wait_if = [&](hipStream_t st, hipEvent_t ev, bool rec) -> int {
         if (rec) CME_TRY(hipStreamWaitEvent(st, ev, 0));

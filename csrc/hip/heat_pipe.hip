@@ -438,6 +438,14 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         R.wave_end[k] = tasks;
     }
     if (R.n == 0) return 0;
+    if (gate.flag && gate.from < R.n) {
+        // the gated (border) workgroups spin until the comm stream's exchange
+        // lands; they are dispatched last, and must leave most resident slots
+        // to the interior and to the exchange's own kernels --
+        // else refuse (the caller falls back to the event schedule)
+        const long gated = tasks - (gate.from > 0 ? R.wave_end[gate.from - 1] : 0);
+        if (2 * gated > resident) return (int)hipErrorInvalidConfiguration;
+    }
     hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR>), dim3(tasks), dim3(NS * WPR * 64), 0, s,
                        prev, curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl, gate);
     CME_LAUNCH_STATUS();

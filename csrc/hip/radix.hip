@@ -20,10 +20,12 @@
 //                writes every digit run contiguously.
 //
 // Hand-offs follow cdna_hip_programming.md §6 G16 R2 ("the data IS the flag"):
-// every (tile, digit) value is ONE 8-byte granule {hi = tag << 2 | state,
-// lo = value} written by one relaxed agent-scope store and re-read by relaxed
-// agent-scope loads until its tag and state are valid; the per-tile status
-// word only tells the poller how far back to look. Tags are unique per pass
+// every (tile, digit) aggregate and inclusive prefix is ONE 8-byte granule
+// {hi = tag << 2 | state, lo = value} (two separate arrays: a granule is
+// written once and never changes meaning while it is summed) written by one
+// relaxed agent-scope store and re-read by relaxed agent-scope loads until
+// its tag and state are valid; the per-tile status word only tells the
+// poller how far back to look. Tags are unique per pass
 // and call (Python hands out the call epoch; under stream capture epoch 0
 // makes the launcher zero the arrays in-stream), so no per-call memset.
 // Grid: co-resident (occupancy API - 1 blocks per CU), block b owns tiles
@@ -129,8 +131,8 @@ template <bool HAS_VALUES>
 __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ vout, long long n, int shift, int mode_in, int mode_out,
-    const uint32_t* __restrict__ counts, uint64_t* __restrict__ gran, uint64_t* __restrict__ stat, int tiles,
-    uint32_t tag, unsigned* timeout) {
+    const uint32_t* __restrict__ counts, uint64_t* __restrict__ agg, uint64_t* __restrict__ inc,
+    uint64_t* __restrict__ stat, int tiles, uint32_t tag, unsigned* timeout) {
     __shared__ uint32_t s_keys[kOsTile];
     __shared__ uint32_t s_vals[HAS_VALUES ? kOsTile : 1];
     __shared__ uint32_t s_cnt[kOsWaves][kBins];  // per-wave running counts, then per-wave exclusive offsets
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
                 s_cnt[w][tid] = cnt;
                 cnt += c;
             }
-            g_store(gran + (size_t)t * kBins + tid, tag, kGAgg, cnt);
+            g_store(agg + (size_t)t * kBins + tid, tag, kGAgg, cnt);
         }
         {
             uint32_t tot;
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int i = i0 + 2 * q;
-                    g[q] = i < K ? g_load(gran + (size_t)(t - 1 - i) * kBins + d) : 0ull;
+                    g[q] = i < K ? g_load(agg + (size_t)(t - 1 - i) * kBins + d) : 0ull;
                 }
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -261,15 +263,15 @@ __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
                     while (g_state(g[q], tag) == 0u) {
                         if (lb_give_up(++spins, timeout, 0)) break;
                         __builtin_amdgcn_s_sleep(1);
-                        g[q] = g_load(gran + (size_t)(t - 1 - i) * kBins + d);
+                        g[q] = g_load(agg + (size_t)(t - 1 - i) * kBins + d);
                     }
                     sum += (uint32_t)g[q];
                 }
             }
             if (h == 1) s_part[d] = sum;
-            uint32_t inc = 0;
+            uint32_t incv = 0;
             if (h == 0 && t - 1 - K >= 0) {  // the inclusive prefix ending the walk
-                const uint64_t* p = gran + (size_t)(t - 1 - K) * kBins + d;
+                const uint64_t* p = inc + (size_t)(t - 1 - K) * kBins + d;
                 uint64_t x = g_load(p);
                 unsigned spins = 0;
                 while (g_state(x, tag) != kGInc) {
@@ -277,15 +279,15 @@ __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
                     __builtin_amdgcn_s_sleep(1);
                     x = g_load(p);
                 }
-                inc = (uint32_t)x;
+                incv = (uint32_t)x;
             }
             __syncthreads();
             if (h == 0) {
-                const uint32_t prefix = inc + sum + s_part[d];
+                const uint32_t prefix = incv + sum + s_part[d];
                 const uint32_t tc = (d + 1 < kBins ? s_off[d + 1] : (uint32_t)min((long long)kOsTile,
                                                                                   n - (long long)t * kOsTile)) -
                                     s_off[d];
-                g_store(gran + (size_t)t * kBins + d, tag, kGInc, prefix + tc);
+                g_store(inc + (size_t)t * kBins + d, tag, kGInc, prefix + tc);
                 s_gb[d] = s_dofs[d] + prefix - s_off[d];
             }
         }
@@ -300,6 +302,7 @@ __global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
         for (int i = tid; i < tile_n; i += kOsThreads) {
             const uint32_t k = s_keys[i];
             const uint32_t g = s_gb[(k >> shift) & 255u] + (uint32_t)i;
+            if ((long long)g >= n) continue;  // only after a look-back timeout: never write out of range
             kout[g] = key_out(k, mode_out);
             if constexpr (HAS_VALUES) vout[g] = s_vals[i];
         }
@@ -319,7 +322,7 @@ int occupancy_blocks_per_cu(K kernel, int threads) {
 // tile status words + (tile, digit) granules.
 CME_EXPORT long long cme_radix_onesweep_ws_bytes(long long n) {
     const long long tiles = (n + kOsTile - 1) / kOsTile;
-    return 2 * kMaxPasses * kBins * 4 + tiles * 8 + tiles * kBins * 8 + 256;
+    return 2 * kMaxPasses * kBins * 4 + tiles * 8 + 2 * tiles * kBins * 8 + 256;
 }
 
 // Sort n keys from kin (not modified) into kout over bits [bit0, bit1) --
@@ -345,7 +348,10 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
     uint32_t* hist = hsets + set * kMaxPasses * kBins;
     uint32_t* hist_next = hsets + (set ^ 1) * kMaxPasses * kBins;
     uint64_t* stat = (uint64_t*)((char*)ws + 2 * kMaxPasses * kBins * 4);
-    uint64_t* gran = stat + tiles;
+    // aggregates and inclusive prefixes in separate arrays: an aggregate
+    // granule never changes meaning while a successor sums it
+    uint64_t* agg = stat + tiles;
+    uint64_t* inc = agg + tiles * kBins;
     if (epoch == 0) {  // captured: zero everything this call reads, every replay
         CME_TRY(hipMemsetAsync(ws, 0, (size_t)cme_radix_onesweep_ws_bytes(n), s));
         hist_next = nullptr;
@@ -377,10 +383,10 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
         const int mi = p == 0 ? mode : 0, mo = p == npass - 1 ? mode : 0;
         if (vin)
             hipLaunchKernelGGL(radix_onesweep_kernel<true>, dim3(grid), dim3(kOsThreads), 0, s, src, dst, vsrc, vdst,
-                               n, shift, mi, mo, hist + p * kBins, gran, stat, (int)tiles, tag, timeout);
+                               n, shift, mi, mo, hist + p * kBins, agg, inc, stat, (int)tiles, tag, timeout);
         else
             hipLaunchKernelGGL(radix_onesweep_kernel<false>, dim3(grid), dim3(kOsThreads), 0, s, src, dst, vsrc,
-                               vdst, n, shift, mi, mo, hist + p * kBins, gran, stat, (int)tiles, tag, timeout);
+                               vdst, n, shift, mi, mo, hist + p * kBins, agg, inc, stat, (int)tiles, tag, timeout);
         CME_TRY(hipGetLastError());
         src = dst;
         vsrc = vdst;

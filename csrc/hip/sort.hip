@@ -366,7 +366,8 @@ __global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_
     __syncthreads();
     const long long i0 = ssplit[0], i1 = ssplit[1];
     const long long j0 = (o0 - a0) - i0, j1 = (o1 - a0) - i1;
-    const int na = (int)(i1 - i0), nb = (int)(j1 - j0);
+    int na = (int)(i1 - i0), nb = (int)(j1 - j0);
+    if (na < 0 || nb < 0 || na + nb > kMsTile || i1 > la || j1 > lb) na = nb = 0;  // never out of range
     for (int x = t; x < na + nb; x += kMsThreads) {
         const bool ia = x < na;
         const long long g = ia ? a0 + i0 + x : a0 + la + j0 + (x - na);
