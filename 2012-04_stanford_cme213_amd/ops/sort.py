@@ -5,10 +5,12 @@ Keys: uint32 natively; int32 and float32 are mapped to order-preserving
 uint32 codes (sign-bit flip / IEEE total-order trick) and back -- inside the
 onesweep kernels (first pass loads, last pass stores), elsewhere by tensor ops.
 
-GPU radix algorithms: "radix" = onesweep (``csrc/hip/radix.hip``: one
-histogram read for every pass, then one read + one write of the keys per
-8-bit digit with decoupled look-back), "radix_rts" = the reduce-then-scan
-form (``csrc/hip/sort.hip``: upsweep + scan + downsweep per digit).
+GPU radix algorithms: "radix" = reduce-then-scan (``csrc/hip/sort.hip``:
+upsweep + one-launch count scan + downsweep per 8-bit digit), "onesweep"
+(``csrc/hip/radix.hip``: one histogram read for every pass, then one read +
+one write of the keys per digit with decoupled look-back across tiles). Both
+are stable and exact; reduce-then-scan is the default because it measures
+faster on MI355X (16M keys: profiles/sort_r3.md).
 """
 from __future__ import annotations
 
@@ -17,6 +19,7 @@ import torch
 from .. import _ext
 
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_sort_u32", "ppppqiipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_radix_sort", "ppppppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_onesweep", "ppppppqiiipqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort", "ppppppqip")
@@ -104,6 +107,33 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
     return (out, vout) if values is not None else out
 
 
+def _rts(keys: torch.Tensor, values: torch.Tensor | None, key_bits: int):
+    """Reduce-then-scan LSD radix sort (cme_radix_sort): key transforms fused
+    into the first and last passes, input untouched."""
+    n = keys.numel()
+    dtype = keys.dtype
+    if dtype not in _MODES:
+        raise TypeError(f"unsupported key dtype {dtype}")
+    if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
+        raise TypeError("key_bits < 32 needs non-negative integer keys")
+    mode = 0 if key_bits < 32 else _MODES[dtype]
+    bits = 32 if key_bits >= 32 else max(1, int(key_bits))
+    k = keys.contiguous()
+    out, tmp = torch.empty_like(k), torch.empty_like(k)
+    vp = vo = vt = None
+    if values is not None:
+        if values.element_size() != 4 or values.numel() != n:
+            raise TypeError("values: one 32-bit value per key")
+        v = values.contiguous()
+        vout, vtmp = torch.empty_like(v), torch.empty_like(v)
+        vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
+    tiles = (n + 4095) // 4096
+    ws = _workspace(keys.device, min(tiles, 4096) * 256 * 4 + 256 * 4 + 256)  # = cme_radix_ws_bytes
+    _ext.call_hip("cme_radix_sort", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, n, mode, 0, bits,
+                  ws.data_ptr(), _ext.stream_ptr(keys.device))
+    return (out, vout) if values is not None else out
+
+
 def _onesweep(keys: torch.Tensor, values: torch.Tensor | None, key_bits: int):
     from .scan import _check_lookback
 
@@ -144,8 +174,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "radix", num_bits: int = 8,
          key_bits: int = 32):
     """Sort a 1-D tensor (optionally carrying int32/uint32/float32 values).
-    GPU algos: "radix" (onesweep, stable), "radix_rts" (reduce-then-scan,
-    stable), "merge". CPU algos: "radix" (OpenMP,
+    GPU algos: "radix" (reduce-then-scan, stable; "radix_rts" is an alias),
+    "onesweep" (decoupled look-back, stable), "merge" (stable). CPU algos: "radix" (OpenMP,
     ``num_bits`` per pass), "radix_serial", "merge" (OpenMP tasks, keys only).
     ``key_bits`` < 32 (GPU radix, non-negative integer keys below
     ``2**key_bits``) runs only the passes covering those bits -- a counting
@@ -154,40 +184,16 @@ def sort(keys: torch.Tensor, values: torch.Tensor | None = None, algo: str = "ra
         raise ValueError("1-D keys expected")
     n = keys.numel()
     dtype = keys.dtype
-    if keys.is_cuda and algo == "radix":
+    if keys.is_cuda and algo in ("radix", "radix_rts", "onesweep"):
         if n <= 1:
             return (keys.clone(), values.clone()) if values is not None else keys.clone()
-        return _onesweep(keys, values, key_bits)
+        if algo == "onesweep":
+            return _onesweep(keys, values, key_bits)
+        return _rts(keys, values, key_bits)
     if keys.is_cuda and algo == "merge":
         return _merge(keys, values)
     if keys.is_cuda:
-        k = _to_u32(keys.contiguous())
-        k2 = torch.empty_like(k)
-        v = v2 = None
-        if values is not None:
-            v = values.contiguous().clone().view(torch.uint32) if values.dtype != torch.uint32 else values.clone()
-            v2 = torch.empty_like(v)
-        s = _ext.stream_ptr(keys.device)
-        vp = v.data_ptr() if v is not None else None
-        v2p = v2.data_ptr() if v2 is not None else None
-        if algo == "radix_rts":
-            ws = _workspace(keys.device, 2 * 1024 * 256 * 4 + 65536)
-            if key_bits < 32 and dtype not in (torch.int32, torch.uint32):
-                raise TypeError("key_bits < 32 needs non-negative integer keys")
-            bits = 32 if key_bits >= 32 else max(1, int(key_bits))
-            if key_bits < 32 and dtype == torch.int32:
-                k = keys.contiguous().clone().view(torch.uint32)  # no sign flip: keys are non-negative
-                k2 = torch.empty_like(k)
-            _ext.call_hip("cme_radix_sort_u32", k.data_ptr(), k2.data_ptr(), vp, v2p, n, 0, bits, ws.data_ptr(), s)
-            if key_bits < 32 and dtype == torch.int32:
-                out = k.view(torch.int32)
-                return (out, v.view(values.dtype)) if values is not None else out
-        else:
-            raise ValueError(algo)
-        out = _from_u32(k, dtype)
-        if values is not None:
-            return out, v.view(values.dtype)
-        return out
+        raise ValueError(f"unknown GPU sort algo {algo!r}")
     if values is not None:
         if algo != "radix":
             raise NotImplementedError("CPU key-value sort: algo='radix'")

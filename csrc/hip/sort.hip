@@ -8,13 +8,20 @@
 // Radix pass (reduce-then-scan structure -- no in-launch hand-offs):
 //   K1 upsweep  : block b histograms its contiguous chunk (LDS atomics) into
 //                 counts[digit * nblocks + b]
-//   K2 scan     : exclusive scan of counts (digit-major) -> global offsets
+//   K2 scan     : one block per digit scans that digit's row of counts over
+//                 the blocks and writes the digit total (one small launch)
 //   K3 downsweep: block b re-reads its chunk tile by tile (4096 keys); keys are
 //                 ranked stably inside each wave with 8 ballots per item
 //                 (wave64 "match"), waves are combined per digit in LDS, the
 //                 tile is reordered by digit in LDS and written out so that
 //                 consecutive lanes store consecutive addresses of a digit run.
-//                 A running per-digit base in LDS carries the chunk across tiles.
+//                 A running per-digit base in LDS carries the chunk across tiles;
+//                 the block's digit bases are the scan of the 256 digit totals
+//                 (done in its prologue) plus its own row prefixes.
+// int32 / float32 keys are mapped to order-preserving uint32 codes by the
+// first pass's loads and back by the last pass's stores (no extra kernels).
+#include <stdlib.h>
+
 #include "cme213/common.h"
 #include "cme213/wave.h"
 
@@ -31,27 +38,65 @@ constexpr int kSortTile = kSortThreads * kItems;  // 4096
 
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift) { return (k >> shift) & (kBins - 1); }
 
+// key codes: 0 uint32, 1 int32 (sign flip), 2 float32 (IEEE order flip)
+__device__ __forceinline__ uint32_t rx_key_in(uint32_t k, int mode) {
+    if (mode == 1) return k ^ 0x80000000u;
+    if (mode == 2) return k ^ ((uint32_t)((int)k >> 31) | 0x80000000u);
+    return k;
+}
+__device__ __forceinline__ uint32_t rx_key_out(uint32_t u, int mode) {
+    if (mode == 1) return u ^ 0x80000000u;
+    if (mode == 2) return u ^ (((uint32_t)((int)u >> 31) ^ 0xffffffffu) | 0x80000000u);
+    return u;
+}
+
 __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint32_t* __restrict__ keys, long long n,
                                                                      long long chunk, int shift, int nblocks,
-                                                                     uint32_t* __restrict__ counts) {
+                                                                     uint32_t* __restrict__ counts, int mode) {
     __shared__ uint32_t hist[kBins];
     for (int i = threadIdx.x; i < kBins; i += kSortThreads) hist[i] = 0;
     __syncthreads();
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    const bool vec = ((uintptr_t)keys & 15u) == 0;  // a tensor view may be 4-B aligned only
     for (long long i = b0 + threadIdx.x * 4; i < b1; i += kSortThreads * 4) {
-        if (i + 3 < b1) {
+        if (vec && i + 3 < b1) {
             const uint4 v = *reinterpret_cast<const uint4*>(keys + i);
-            atomicAdd(&hist[digit_of(v.x, shift)], 1u);
-            atomicAdd(&hist[digit_of(v.y, shift)], 1u);
-            atomicAdd(&hist[digit_of(v.z, shift)], 1u);
-            atomicAdd(&hist[digit_of(v.w, shift)], 1u);
+            atomicAdd(&hist[digit_of(rx_key_in(v.x, mode), shift)], 1u);
+            atomicAdd(&hist[digit_of(rx_key_in(v.y, mode), shift)], 1u);
+            atomicAdd(&hist[digit_of(rx_key_in(v.z, mode), shift)], 1u);
+            atomicAdd(&hist[digit_of(rx_key_in(v.w, mode), shift)], 1u);
         } else {
-            for (long long j = i; j < b1; ++j) atomicAdd(&hist[digit_of(keys[j], shift)], 1u);
+            for (long long j = i; j < b1 && j < i + 4; ++j) atomicAdd(&hist[digit_of(rx_key_in(keys[j], mode), shift)], 1u);
         }
     }
     __syncthreads();
     for (int d = threadIdx.x; d < kBins; d += kSortThreads) counts[(size_t)d * nblocks + blockIdx.x] = hist[d];
+}
+
+// K2: block d scans row d of counts (nblocks <= kMaxRadixBlocks values, R
+// consecutive per lane) in place to exclusive prefixes and writes the total
+constexpr int kMaxRadixBlocks = 4096;
+__global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__ counts, int nblocks,
+                                                          uint32_t* __restrict__ totals) {
+    constexpr int R = kMaxRadixBlocks / 1024;
+    __shared__ uint32_t tmp[16];
+    const int d = blockIdx.x, b0 = threadIdx.x * R;
+    uint32_t* row = counts + (size_t)d * nblocks;
+    uint32_t c[R], sum = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        c[r] = b0 + r < nblocks ? row[b0 + r] : 0u;
+        sum += c[r];
+    }
+    uint32_t tot;
+    uint32_t ex = block_exclusive_scan<16>(sum, tmp, tot, OpAdd());
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (b0 + r < nblocks) row[b0 + r] = ex;
+        ex += c[r];
+    }
+    if (threadIdx.x == 0) totals[d] = tot;
 }
 
 // Stable rank of each lane's digit among the lanes of its wave (ballot match).
@@ -69,7 +114,7 @@ template <bool HAS_VALUES>
 __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
     const uint32_t* __restrict__ keys_in, uint32_t* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, long long n, long long chunk, int shift, int nblocks,
-    const uint32_t* __restrict__ offsets) {
+    const uint32_t* __restrict__ prefix, const uint32_t* __restrict__ totals, int mode_in, int mode_out) {
     __shared__ uint32_t s_keys[kSortTile];
     __shared__ uint32_t s_vals[HAS_VALUES ? kSortTile : 1];
     __shared__ uint32_t s_whist[kSortWaves][kBins];  // per-wave running counts, then exclusive prefixes
@@ -79,7 +124,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
     const int wid = threadIdx.x / kWave;
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
-    for (int d = threadIdx.x; d < kBins; d += kSortThreads) s_base[d] = offsets[(size_t)d * nblocks + blockIdx.x];
+    {  // digit bases: scan of the digit totals + this block's row prefix
+        __shared__ uint32_t s_t[kSortWaves];
+        uint32_t tot;
+        const uint32_t db = block_exclusive_scan<kSortWaves>(totals[threadIdx.x], s_t, tot, OpAdd());
+        s_base[threadIdx.x] = db + prefix[(size_t)threadIdx.x * nblocks + blockIdx.x];
+    }
 
     for (long long t0 = b0; t0 < b1; t0 += kSortTile) {
         for (int d = threadIdx.x; d < kBins; d += kSortThreads)
@@ -93,7 +143,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
         for (int k = 0; k < kItems; ++k) {
             const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
             const bool ok = i < b1;
-            key[k] = ok ? keys_in[i] : 0xffffffffu;
+            key[k] = ok ? rx_key_in(keys_in[i], mode_in) : 0xffffffffu;
             if constexpr (HAS_VALUES) val[k] = ok ? vals_in[i] : 0u;
         }
 #pragma unroll
@@ -108,6 +158,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
             // the lowest lane of each peer group publishes the new running count
             if (ok && below == 0) s_whist[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
             if (!ok) rank[k] = 0xffffffffu;
+            __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its LDS update
         }
         __syncthreads();
         // per digit: exclusive prefix across waves, tile totals, tile offsets
@@ -148,7 +199,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
             const uint32_t k = s_keys[i];
             const uint32_t d = digit_of(k, shift);
             const uint32_t g = s_base[d] + (uint32_t)i - s_tile_off[d];
-            keys_out[g] = k;
+            keys_out[g] = rx_key_out(k, mode_out);
             if constexpr (HAS_VALUES) vals_out[g] = s_vals[i];
         }
         __syncthreads();
@@ -166,10 +217,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
 // Stable merge sort in two kernels (wave64, LDS-staged; the hw4 merge sort's
 // median split + upper_bound merge, hw/hw4/programming/mergesort.cpp:31-144,
 // becomes a merge-path split):
-//   block sort : a 256-lane block sorts a 4096-key tile: 16 consecutive keys
+//   block sort : a 512-lane block sorts an 8192-key tile: 16 consecutive keys
 //                per lane sorted in registers by odd-even transposition
-//                (stable), then 8 rounds of merge path in LDS (runs of 16 ->
-//                4096, A first on ties: stable);
+//                (stable), then 9 rounds of merge path in LDS (runs of 16 ->
+//                8192, A first on ties: stable; LDS padded one word per 16);
 //   merge pass : output tile o (4096 keys) of a pass merging runs of L: the
 //                block finds its two diagonal splits by a cooperative 128-ary
 //                search (2 x 128 lanes, ~4 dependent rounds of global loads
@@ -178,9 +229,17 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
 //                stores the tile coalesced through LDS.
 // Keys are uint32 codes (int32 / float32 mapped on the block sort's loads and
 // back on the last pass's stores, as the radix sort does). Values optional.
-constexpr int kMsThreads = 256;
+constexpr int kMsThreads = 256;                  // merge pass: 4096-key output tiles
 constexpr int kMsItems = 16;
-constexpr int kMsTile = kMsThreads * kMsItems;  // 4096
+constexpr int kMsTile = kMsThreads * kMsItems;    // 4096
+constexpr int kBsThreads = 512;                   // block sort: 8192-key tiles (one pass fewer)
+constexpr int kBsTile = kBsThreads * kMsItems;    // 8192
+
+// LDS index padding: one pad word per 16, so lane t's run [16t, 16t+16)
+// starts at bank 17t mod 32 -- the per-lane 16-strided accesses (lane-major
+// loads/stores of register runs) are conflict-free (unpadded: 16-way)
+__device__ __forceinline__ int lp(int i) { return i + (i >> 4); }
+constexpr int lp_size(int n) { return n + n / 16; }
 
 __device__ __forceinline__ uint32_t ms_key_in(uint32_t k, int mode) {
     if (mode == 1) return k ^ 0x80000000u;
@@ -193,9 +252,8 @@ __device__ __forceinline__ uint32_t ms_key_out(uint32_t u, int mode) {
     return u;
 }
 
-// merge-path split of diagonal `diag` between A[0, la) and B[0, lb) (LDS or
-// registers-free generic accessor): number of A elements among the first
-// `diag` outputs, A first on ties
+// merge-path split of diagonal `diag` between A[0, la) and B[0, lb):
+// number of A elements among the first `diag` outputs, A first on ties
 template <typename FA, typename FB>
 __device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
     int lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
@@ -207,31 +265,32 @@ __device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
     return lo;
 }
 
-// sequential merge of `cnt` outputs from A[i..la) / B[j..lb) (LDS) into registers
-template <bool HAS_VALUES>
+// sequential merge of kMsItems outputs from A = [a0, a0+la) / B = [b0, b0+lb)
+// (logical LDS indices, padded on access) into registers
+template <bool HAS_VALUES, int CAP>
 __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* sv, int a0, int la, int b0, int lb,
                                            int i, int j, uint32_t (&k)[kMsItems], uint32_t (&v)[kMsItems]) {
-    uint32_t ka = i < la ? sk[a0 + i] : 0xffffffffu, kb = j < lb ? sk[b0 + j] : 0xffffffffu;
+    uint32_t ka = i < la ? sk[lp(a0 + i)] : 0xffffffffu, kb = j < lb ? sk[lp(b0 + j)] : 0xffffffffu;
 #pragma unroll
     for (int q = 0; q < kMsItems; ++q) {
         const bool take_a = j >= lb || (i < la && ka <= kb);
         k[q] = take_a ? ka : kb;
         if constexpr (HAS_VALUES) {
             const int x = take_a ? a0 + i : b0 + j;  // past both ends only on padding lanes
-            v[q] = sv[x < kMsTile ? x : kMsTile - 1];
+            v[q] = sv[lp(x < CAP ? x : CAP - 1)];
         }
         if (take_a) {
             ++i;
-            ka = i < la ? sk[a0 + i] : 0xffffffffu;
+            ka = i < la ? sk[lp(a0 + i)] : 0xffffffffu;
         } else {
             ++j;
-            kb = j < lb ? sk[b0 + j] : 0xffffffffu;
+            kb = j < lb ? sk[lp(b0 + j)] : 0xffffffffu;
         }
     }
 }
 
 // coalesced tile store through LDS: lane t holds outputs [16t, 16t+16)
-template <bool HAS_VALUES>
+template <bool HAS_VALUES, int NT>
 __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const uint32_t (&k)[kMsItems],
                                               const uint32_t (&v)[kMsItems], uint32_t* __restrict__ ko,
                                               uint32_t* __restrict__ vo, long long base, int cnt, int mode) {
@@ -239,38 +298,38 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
     const int t = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < kMsItems; ++q) {
-        sk[kMsItems * t + q] = k[q];
-        if constexpr (HAS_VALUES) sv[kMsItems * t + q] = v[q];
+        sk[lp(kMsItems * t + q)] = k[q];
+        if constexpr (HAS_VALUES) sv[lp(kMsItems * t + q)] = v[q];
     }
     __syncthreads();
-    for (int i = t; i < cnt; i += kMsThreads) {
-        ko[base + i] = ms_key_out(sk[i], mode);
-        if constexpr (HAS_VALUES) vo[base + i] = sv[i];
+    for (int i = t; i < cnt; i += NT) {
+        ko[base + i] = ms_key_out(sk[lp(i)], mode);
+        if constexpr (HAS_VALUES) vo[base + i] = sv[lp(i)];
     }
 }
 
 template <bool HAS_VALUES>
-__global__ __launch_bounds__(kMsThreads) void ms_block_sort_kernel(const uint32_t* __restrict__ ki,
+__global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_t* __restrict__ ki,
                                                                    uint32_t* __restrict__ ko,
                                                                    const uint32_t* __restrict__ vi,
                                                                    uint32_t* __restrict__ vo, long long n,
                                                                    int mode_in, int mode_out) {
-    __shared__ uint32_t sk[kMsTile];
-    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
+    __shared__ uint32_t sk[lp_size(kBsTile)];
+    __shared__ uint32_t sv[HAS_VALUES ? lp_size(kBsTile) : 1];
     const int t = threadIdx.x;
-    const long long base = (long long)blockIdx.x * kMsTile;
-    const int cnt = (int)(n - base < kMsTile ? n - base : kMsTile);
+    const long long base = (long long)blockIdx.x * kBsTile;
+    const int cnt = (int)(n - base < kBsTile ? n - base : kBsTile);
     // coalesced load into LDS, then lane t takes keys [16t, 16t+16)
-    for (int i = t; i < kMsTile; i += kMsThreads) {
-        sk[i] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
-        if constexpr (HAS_VALUES) sv[i] = i < cnt ? vi[base + i] : 0u;
+    for (int i = t; i < kBsTile; i += kBsThreads) {
+        sk[lp(i)] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
+        if constexpr (HAS_VALUES) sv[lp(i)] = i < cnt ? vi[base + i] : 0u;
     }
     __syncthreads();
     uint32_t k[kMsItems], v[kMsItems];
 #pragma unroll
     for (int q = 0; q < kMsItems; ++q) {
-        k[q] = sk[kMsItems * t + q];
-        if constexpr (HAS_VALUES) v[q] = sv[kMsItems * t + q];
+        k[q] = sk[lp(kMsItems * t + q)];
+        if constexpr (HAS_VALUES) v[q] = sv[lp(kMsItems * t + q)];
     }
     // odd-even transposition: swaps only strictly greater neighbours (stable);
     // padding keys (all ones) sit at the tile's end and stay behind real keys
@@ -291,21 +350,22 @@ __global__ __launch_bounds__(kMsThreads) void ms_block_sort_kernel(const uint32_
         }
     }
     // merge rounds in LDS: runs of 16 << r
-    for (int L = kMsItems; L < kMsTile; L <<= 1) {
+    for (int L = kMsItems; L < kBsTile; L <<= 1) {
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kMsItems; ++q) {
-            sk[kMsItems * t + q] = k[q];
-            if constexpr (HAS_VALUES) sv[kMsItems * t + q] = v[q];
+            sk[lp(kMsItems * t + q)] = k[q];
+            if constexpr (HAS_VALUES) sv[lp(kMsItems * t + q)] = v[q];
         }
         __syncthreads();
         const int out0 = kMsItems * t;
         const int a0 = out0 & ~(2 * L - 1), b0 = a0 + L;
         const int diag = out0 - a0;
-        const int i = ms_split([&](int x) { return sk[a0 + x]; }, [&](int x) { return sk[b0 + x]; }, L, L, diag);
-        ms_merge16<HAS_VALUES>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
+        const int i = ms_split([&](int x) { return sk[lp(a0 + x)]; }, [&](int x) { return sk[lp(b0 + x)]; }, L, L,
+                               diag);
+        ms_merge16<HAS_VALUES, kBsTile>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
     }
-    ms_store_tile<HAS_VALUES>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
+    ms_store_tile<HAS_VALUES, kBsThreads>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -345,12 +405,14 @@ __global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_
                                                                    const uint32_t* __restrict__ vi,
                                                                    uint32_t* __restrict__ vo, long long n,
                                                                    long long L, int mode_out) {
-    __shared__ uint32_t sk[kMsTile];
-    __shared__ uint32_t sv[HAS_VALUES ? kMsTile : 1];
+    __shared__ uint32_t sk[lp_size(kMsTile)];
+    __shared__ uint32_t sv[HAS_VALUES ? lp_size(kMsTile) : 1];
     __shared__ uint64_t smask[2][2];
     __shared__ long long ssplit[2];
     const int t = threadIdx.x;
-    const long long o0 = (long long)blockIdx.x * kMsTile;
+    // consecutive output tiles on one XCD: their diagonal searches probe the
+    // same lines of A and B, which then hit that XCD's L2
+    const long long o0 = (long long)xcd_remap(blockIdx.x, gridDim.x) * kMsTile;
     const long long o1 = o0 + kMsTile < n ? o0 + kMsTile : n;
     const long long a0 = o0 & ~(2 * L - 1);  // pair start (2L is a multiple of the tile)
     const long long la = a0 + L < n ? L : n - a0;
@@ -371,69 +433,96 @@ __global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_
     for (int x = t; x < na + nb; x += kMsThreads) {
         const bool ia = x < na;
         const long long g = ia ? a0 + i0 + x : a0 + la + j0 + (x - na);
-        sk[x] = ki[g];
-        if constexpr (HAS_VALUES) sv[x] = vi[g];
+        sk[lp(x)] = ki[g];
+        if constexpr (HAS_VALUES) sv[lp(x)] = vi[g];
     }
     __syncthreads();
     const int cnt = na + nb;
     const int diag_l = kMsItems * t < cnt ? kMsItems * t : cnt;
-    const int i = ms_split([&](int x) { return sk[x]; }, [&](int x) { return sk[na + x]; }, na, nb, diag_l);
+    const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int x) { return sk[lp(na + x)]; }, na, nb, diag_l);
     uint32_t k[kMsItems], v[kMsItems];
-    ms_merge16<HAS_VALUES>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
-    ms_store_tile<HAS_VALUES>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
+    ms_merge16<HAS_VALUES, kMsTile>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
+    ms_store_tile<HAS_VALUES, kMsThreads>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
 }
 
 }  // namespace
 
-CME_EXPORT long long cme_radix_ws_bytes(long long n) {
-    long long tiles = (n + kSortTile - 1) / kSortTile;
-    long long nb = tiles < 1024 ? tiles : 1024;
-    return nb * kBins * 4 * 2 + 65536;
+// blocks of the upsweep / downsweep grid: at most 1024 (4 per CU), each
+// walking several 4096-key tiles -- measured on MI355X, 16M keys: 0.357 /
+// 0.363 / 0.391 ms at caps 1024 / 2048 / 4096 (48M: 1.18 / 1.13 / 1.14).
+// CME_RADIX_MAXBLOCKS overrides the cap (<= kMaxRadixBlocks, sweeps).
+static int radix_max_blocks() {
+    static const int v = [] {
+        const char* e = getenv("CME_RADIX_MAXBLOCKS");
+        int x = e ? atoi(e) : 1024;
+        return x < 1 ? 1 : (x > kMaxRadixBlocks ? kMaxRadixBlocks : x);
+    }();
+    return v;
 }
 
-// from scan.hip (reduce-then-scan, deterministic)
-extern "C" int cme_scan_rts(const void* in, void* out, long long n, int dtype, int exclusive, void* ws, void* stream);
+CME_EXPORT long long cme_radix_ws_bytes(long long n) {
+    long long tiles = (n + kSortTile - 1) / kSortTile;
+    long long nb = tiles < kMaxRadixBlocks ? tiles : kMaxRadixBlocks;
+    return nb * kBins * 4 + kBins * 4 + 256;
+}
 
-// LSD radix sort of uint32 keys (and optional uint32 values) over bits
-// [bit0, bit1). Ping-pongs between (keys, keys_alt); the sorted output is
-// left in `keys` (copied back after an odd number of passes).
+// LSD radix sort of n keys from `in` (not modified) into `out` over bits
+// [bit0, bit1), ping-ponging through `tmp` so that the last pass writes out;
+// values (optional) likewise. mode: 0 uint32, 1 int32, 2 float32 keys.
 // ws: cme_radix_ws_bytes(n) bytes.
-CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, long long n,
-                                  int bit0, int bit1, void* ws, void* stream) {
+CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
+                              uint32_t* vtmp, long long n, int mode, int bit0, int bit1, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
-    if (n <= 1) return 0;
+    if (n <= 0) return 0;
+    if (bit0 < 0 || bit1 > 32 || bit1 <= bit0 || mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) ||
+        (vin && !vtmp) || n >= (1ll << 32))
+        return (int)hipErrorInvalidValue;
     const long long tiles = (n + kSortTile - 1) / kSortTile;
-    int nb = tiles < 1024 ? (int)tiles : 1024;
+    const int cap = radix_max_blocks();
+    int nb = tiles < cap ? (int)tiles : cap;
     const long long chunk = ((tiles + nb - 1) / nb) * kSortTile;
     nb = (int)((n + chunk - 1) / chunk);
     uint32_t* counts = (uint32_t*)ws;
-    uint32_t* offs = counts + (size_t)nb * kBins;
-    void* scan_ws = offs + (size_t)nb * kBins;
-    uint32_t *ki = keys, *ko = keys_alt, *vi = vals, *vo = vals_alt;
-    int passes = 0;
-    for (int shift = bit0; shift < bit1; shift += kRadixBits, ++passes) {
-        hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts);
-        int rc = cme_scan_rts(counts, offs, (long long)nb * kBins, 2, 1, scan_ws, stream);
-        if (rc) return rc;
-        if (vals)
+    uint32_t* totals = counts + (size_t)nb * kBins;
+    const int npass = (bit1 - bit0 + kRadixBits - 1) / kRadixBits;
+    const uint32_t* ki = in;
+    const uint32_t* vi = vin;
+    for (int p = 0; p < npass; ++p) {
+        const bool to_out = ((npass - 1 - p) & 1) == 0;  // the last pass lands in out
+        uint32_t* ko = to_out ? out : tmp;
+        uint32_t* vo = vin ? (to_out ? vout : vtmp) : nullptr;
+        const int shift = bit0 + kRadixBits * p;
+        const int mi = p == 0 ? mode : 0, mo = p == npass - 1 ? mode : 0;
+        hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts,
+                           mi);
+        hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins), dim3(1024), 0, s, counts, nb, totals);
+        if (vin)
             hipLaunchKernelGGL(radix_downsweep_kernel<true>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
-                               chunk, shift, nb, offs);
+                               chunk, shift, nb, counts, totals, mi, mo);
         else
             hipLaunchKernelGGL(radix_downsweep_kernel<false>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
-                               chunk, shift, nb, offs);
+                               chunk, shift, nb, counts, totals, mi, mo);
         CME_TRY(hipGetLastError());
-        uint32_t* t = ki;
         ki = ko;
-        ko = t;
-        t = vi;
         vi = vo;
-        vo = t;
     }
-    if (passes & 1) {
-        CME_TRY(hipMemcpyAsync(keys, ki, n * 4, hipMemcpyDeviceToDevice, s));
-        if (vals) CME_TRY(hipMemcpyAsync(vals, vi, n * 4, hipMemcpyDeviceToDevice, s));
+    return 0;
+}
+
+// In-place form (sorted uint32 keys left in `keys`; keys_alt / vals_alt scratch).
+CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* vals, uint32_t* vals_alt, long long n,
+                                  int bit0, int bit1, void* ws, void* stream) {
+    if (n <= 1) return 0;
+    const int npass = (bit1 - bit0 + kRadixBits - 1) / kRadixBits;
+    if (npass & 1) {  // odd: sort into keys_alt, copy back
+        int rc = cme_radix_sort(keys, keys_alt, keys, vals, vals ? vals_alt : nullptr, vals, n, 0, bit0, bit1, ws,
+                                stream);
+        if (rc) return rc;
+        CME_TRY(hipMemcpyAsync(keys, keys_alt, n * 4, hipMemcpyDeviceToDevice, as_stream(stream)));
+        if (vals) CME_TRY(hipMemcpyAsync(vals, vals_alt, n * 4, hipMemcpyDeviceToDevice, as_stream(stream)));
+        return 0;
     }
-    CME_LAUNCH_STATUS();
+    return cme_radix_sort(keys, keys, keys_alt, vals, vals, vals_alt, n, 0, bit0, bit1, ws, stream);
 }
 
 // Stable merge sort of n keys from `in` into `out` (ping-pong through `tmp`;
@@ -446,21 +535,21 @@ CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     if (mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) || (vin && !vtmp))
         return (int)hipErrorInvalidValue;
     int npass = 0;
-    for (long long L = kMsTile; L < n; L <<= 1) ++npass;
+    for (long long L = kBsTile; L < n; L <<= 1) ++npass;
     // the block sort writes where an even number of passes later lands in out
     uint32_t* d0 = (npass & 1) ? tmp : out;
     uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
-    const unsigned tiles = cdiv(n, kMsTile);
+    const unsigned btiles = cdiv(n, kBsTile), tiles = cdiv(n, kMsTile);
     if (vin)
-        hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, in, d0, vin, v0, n, mode,
+        hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode,
                            npass ? 0 : mode);
     else
-        hipLaunchKernelGGL(ms_block_sort_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, in, d0, vin, v0, n, mode,
-                           npass ? 0 : mode);
+        hipLaunchKernelGGL(ms_block_sort_kernel<false>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n,
+                           mode, npass ? 0 : mode);
     CME_TRY(hipGetLastError());
     const uint32_t *ki = d0, *vi = v0;
     int p = 0;
-    for (long long L = kMsTile; L < n; L <<= 1, ++p) {
+    for (long long L = kBsTile; L < n; L <<= 1, ++p) {
         const bool last = p == npass - 1;
         uint32_t* ko = (ki == out) ? tmp : out;
         uint32_t* vo = vin ? ((vi == vout) ? vtmp : vout) : nullptr;
@@ -486,5 +575,5 @@ CME_EXPORT int cme_merge_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel);
 CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
-CME_REGISTER_KERNEL(ms_block_sort, 256, ms_block_sort_kernel<false>);
+CME_REGISTER_KERNEL(ms_block_sort, 512, ms_block_sort_kernel<false>);
 CME_REGISTER_KERNEL(ms_merge_pass, 256, ms_merge_pass_kernel<false>);

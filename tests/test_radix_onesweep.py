@@ -1,4 +1,5 @@
-"""Onesweep radix sort (csrc/hip/radix.hip): exact against torch.sort for
+"""GPU radix sorts -- reduce-then-scan ("radix", csrc/hip/sort.hip) and
+onesweep ("onesweep", csrc/hip/radix.hip) -- and the merge sort: exact against torch.sort for
 every key type, tile-boundary sizes, skewed digit distributions (all keys
 equal: one digit run per pass; sorted / reversed inputs: look-back chains of
 one digit), key-value stability, bit-limited sorts, misaligned views, and
@@ -54,9 +55,10 @@ def _from_gpu(y, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 1000, TILE - 1, TILE, TILE + 1, 5 * TILE + 17, 1_000_003, 4 * 1024 * 1024 + 3])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.uint32, torch.float32])
-def test_onesweep_random(gpu, n, dtype):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_random(gpu, algo, n, dtype):
     x = _keys(n, dtype, "random", seed=n)
-    y = _from_gpu(sort(_to_gpu(x, dtype, gpu)), dtype)
+    y = _from_gpu(sort(_to_gpu(x, dtype, gpu), algo=algo), dtype)
     assert torch.equal(y, torch.sort(x).values)
     assert not lookback_timed_out(gpu)
 
@@ -64,44 +66,48 @@ def test_onesweep_random(gpu, n, dtype):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["equal", "sorted", "reversed", "fewbits"])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
-def test_onesweep_skewed(gpu, kind, dtype):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_skewed(gpu, algo, kind, dtype):
     n = 3 * 1024 * 1024 + 5
     x = _keys(n, dtype, kind)
-    y = sort(x.to(gpu)).cpu()
+    y = sort(x.to(gpu), algo=algo).cpu()
     assert torch.equal(y, torch.sort(x).values)
     assert not lookback_timed_out(gpu)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [777, 2_000_001])
-def test_onesweep_key_value_stable(gpu, n):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_key_value_stable(gpu, algo, n):
     k = torch.randint(0, 300, (n,), dtype=torch.int32)  # long equal-key runs across tiles
     v = torch.arange(n, dtype=torch.int32)
-    ks, vs = sort(k.to(gpu), v.to(gpu))
+    ks, vs = sort(k.to(gpu), v.to(gpu), algo=algo)
     ref = torch.sort(k, stable=True)
     assert torch.equal(ks.cpu(), ref.values) and torch.equal(vs.cpu(), ref.indices.to(torch.int32))
     f = torch.randn(n)
-    fs, fv = sort(f.to(gpu), v.to(gpu))
+    fs, fv = sort(f.to(gpu), v.to(gpu), algo=algo)
     ref = torch.sort(f, stable=True)
     assert torch.equal(fs.cpu(), ref.values) and torch.equal(fv.cpu(), ref.indices.to(torch.int32))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", [1, 8, 12, 20, 31])
-def test_onesweep_key_bits(gpu, bits):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_key_bits(gpu, algo, bits):
     n = 600_001
     k = torch.randint(0, 2**bits, (n,), dtype=torch.int64).to(torch.int32)
     v = torch.arange(n, dtype=torch.int32)
-    ks, vs = sort(k.to(gpu), v.to(gpu), key_bits=bits)
+    ks, vs = sort(k.to(gpu), v.to(gpu), key_bits=bits, algo=algo)
     ref = torch.sort(k, stable=True)
     assert torch.equal(ks.cpu(), ref.values) and torch.equal(vs.cpu(), ref.indices.to(torch.int32))
 
 
 @pytest.mark.gpu
-def test_onesweep_misaligned_view_and_input_untouched(gpu):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_misaligned_view_and_input_untouched(gpu, algo):
     x = torch.randint(-2**31, 2**31 - 1, (100_003,), dtype=torch.int32).to(gpu)
     before = x.clone()
-    y = sort(x[1:])  # 4-byte offset: the histogram pass must not use 16-B loads
+    y = sort(x[1:], algo=algo)  # 4-byte offset: the histogram pass must not use 16-B loads
     assert torch.equal(y.cpu(), torch.sort(before[1:].cpu()).values)
     assert torch.equal(x, before)
 
@@ -109,27 +115,28 @@ def test_onesweep_misaligned_view_and_input_untouched(gpu):
 @pytest.mark.gpu
 def test_onesweep_many_calls_and_algos_agree(gpu):
     """Epoch-tagged workspace reused across calls (no memset): 30 calls of
-    varying sizes, each checked; the reduce-then-scan algorithm agrees."""
+    varying sizes, each checked; the onesweep algorithm agrees."""
     for i in range(30):
         n = 1 + (i * 37_313) % 300_000
         x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, generator=torch.Generator().manual_seed(i))
         xg = x.to(gpu)
         a = sort(xg)
-        b = sort(xg, algo="radix_rts")
+        b = sort(xg, algo="onesweep")
         assert torch.equal(a, b)
         assert torch.equal(a.cpu(), torch.sort(x).values)
 
 
 @pytest.mark.gpu
-def test_onesweep_graph_capture(gpu):
+@pytest.mark.parametrize("algo", ["radix", "onesweep"])
+def test_onesweep_graph_capture(gpu, algo):
     n = 1_234_567
     x = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32).to(gpu)
-    sort(x)  # warm-up outside capture
+    sort(x, algo=algo)  # warm-up outside capture
     s = torch.cuda.Stream(gpu)
     s.wait_stream(torch.cuda.current_stream(gpu))
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        y = sort(x)
+        y = sort(x, algo=algo)
     for seed in (1, 2):
         x.copy_(torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, generator=torch.Generator().manual_seed(seed)))
         g.replay()
@@ -142,7 +149,7 @@ MS_TILE = 4096
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 2, 17, MS_TILE - 1, MS_TILE, MS_TILE + 1, 3 * MS_TILE + 5, 8 * MS_TILE,
+@pytest.mark.parametrize("n", [1, 2, 17, MS_TILE - 1, MS_TILE, MS_TILE + 1, 2 * MS_TILE - 1, 2 * MS_TILE + 1, 3 * MS_TILE + 5, 8 * MS_TILE,
                                1_000_003, 5 * 1024 * 1024 + 7])
 @pytest.mark.parametrize("dtype", [torch.int32, torch.uint32, torch.float32])
 def test_merge_sort_sizes(gpu, n, dtype):
