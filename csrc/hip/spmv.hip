@@ -67,7 +67,13 @@ __global__ __launch_bounds__(256) void csr_vector_kernel(int nrows, const int* _
     if (r < nrows && sub == 0) y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
 
-template <int G>
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// NT: the column / value stream is read with non-temporal loads, so it does
+// not evict the gathered vector x from L2 (a 1M-column fp32 x is 4 MB, one
+// XCD's L2): the random gathers then hit L2 instead of the Infinity Cache
+template <int G, bool NT>
 __global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __restrict__ rp,
                                                        const int* __restrict__ col, const float* __restrict__ val,
                                                        const float* __restrict__ x, float* __restrict__ y,
@@ -78,8 +84,15 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __r
     if (r < nrows) {
         const int b = rp[r], e = rp[r + 1];  // multiples of 4 (aligned CSR)
         for (int j = b + 4 * sub; j < e; j += 4 * G) {
-            const int4 c = *reinterpret_cast<const int4*>(col + j);
-            const float4 v = *reinterpret_cast<const float4*>(val + j);
+            i32x4 c;
+            f32x4 v;
+            if constexpr (NT) {
+                c = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(col + j));
+                v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(val + j));
+            } else {
+                c = *reinterpret_cast<const i32x4*>(col + j);
+                v = *reinterpret_cast<const f32x4*>(val + j);
+            }
             s += v.x * x[c.x] + v.y * x[c.y] + v.z * x[c.z] + v.w * x[c.w];
         }
     }
@@ -294,8 +307,21 @@ CME_EXPORT int cme_spmv_csr_aligned(int nrows, const int* rp, const int* col, co
                                     float* y, int group, float beta, void* stream) {
     hipStream_t s = as_stream(stream);
     if (((uintptr_t)col % 16) || ((uintptr_t)val % 16)) return (int)hipErrorInvalidValue;
+    // CME_SPMV_NT=0/1 selects the stream loads (default: non-temporal)
+    static const bool nt = [] {
+        const char* e = getenv("CME_SPMV_NT");
+        return e ? atoi(e) != 0 : true;
+    }();
     switch (group) {
-#define V(G) case G: hipLaunchKernelGGL(csr_vec4_kernel<G>, dim3(cdiv((size_t)nrows * G, 256)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+#define V(G)                                                                                                      \
+    case G:                                                                                                       \
+        if (nt)                                                                                                   \
+            hipLaunchKernelGGL((csr_vec4_kernel<G, true>), dim3(cdiv((size_t)nrows * G, 256)), dim3(256), 0, s,    \
+                               nrows, rp, col, val, x, y, beta);                                                  \
+        else                                                                                                      \
+            hipLaunchKernelGGL((csr_vec4_kernel<G, false>), dim3(cdiv((size_t)nrows * G, 256)), dim3(256), 0, s,   \
+                               nrows, rp, col, val, x, y, beta);                                                  \
+        break;
         V(1) V(2) V(4) V(8) V(16) V(32) V(64)
 #undef V
         default: return (int)hipErrorInvalidValue;
@@ -342,7 +368,7 @@ CME_EXPORT int cme_spmv_coo(int nrows, long long nnz, const int* row, const int*
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(spmv_csr_scalar, 256, csr_scalar_kernel);
 CME_REGISTER_KERNEL(spmv_csr_vector8, 256, csr_vector_kernel<8>);
-CME_REGISTER_KERNEL(spmv_csr_aligned4, 256, csr_vec4_kernel<4>);
+CME_REGISTER_KERNEL(spmv_csr_aligned4, 256, csr_vec4_kernel<4, true>);
 CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);
 CME_REGISTER_KERNEL(spmv_dia, 256, dia_kernel);
 CME_REGISTER_KERNEL(spmv_dia4, 256, dia4_kernel);
