@@ -1,7 +1,7 @@
 """hw1 drivers: ``cipher [book]`` and ``pagerank`` (+ the analysis sweeps).
 
     python -m cme213x cipher [mobydick.txt] [--sweep vl|bs]
-    python -m cme213x pagerank [--avg-edges 8] [--group 1] [--sweep]
+    python -m cme213x pagerank [--avg-edges 8] [--group 1] [--blocks 0] [--sweep]
 """
 from __future__ import annotations
 
@@ -39,11 +39,12 @@ def pagerank_main(argv=None) -> int:
     ap.add_argument("--avg-edges", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--group", type=int, default=1)
+    ap.add_argument("--blocks", type=int, default=0, help="column-blocked sweeps (2 = fastest measured)")
     ap.add_argument("--sweep", action="store_true")
     a = ap.parse_args(argv)
     if a.sweep:
         for r in sweep_avg_edges(a.nodes, iters=a.iters, group=a.group):
             print(f"{r['avg_edges']},{r['ms']:.2f},{r['bytes']},{r['GBps']:.4f}")
         return 0
-    res = run_hw1_pagerank(a.nodes, a.avg_edges, a.iters, group=a.group)
+    res = run_hw1_pagerank(a.nodes, a.avg_edges, a.iters, group=a.group, blocks=a.blocks)
     return 1 if res.get("errors") else 0

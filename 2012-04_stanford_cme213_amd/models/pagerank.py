@@ -17,7 +17,10 @@ from ..utils.ulp import ulp_distance
 
 
 def run_hw1_pagerank(n: int = 1 << 21, avg_edges: int = 8, iters: int = 20, device: str | None = None,
-                     group: int = 1, max_ulps: int = 10, seed: int = 0) -> dict:
+                     group: int = 1, max_ulps: int = 10, seed: int = 0, blocks: int = 0) -> dict:
+    """``blocks`` > 1: column-blocked sweeps (``ops.graph.block_columns``;
+    fastest measured: blocks 2, group 2 -- profiles/pagerank_r3.md). The
+    default (group 1, unblocked) keeps the CPU summation order bit for bit."""
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
     g = make_graph(n, avg_edges, seed)
     x0 = torch.full((n,), 1.0 / n, dtype=torch.float32)
@@ -25,6 +28,10 @@ def run_hw1_pagerank(n: int = 1 << 21, avg_edges: int = 8, iters: int = 20, devi
     if device != "cpu":
         dev = torch.device(device)
         gd = g.to(dev)
+        if blocks > 1:
+            from ..ops.graph import block_columns
+
+            gd = block_columns(gd, blocks)
         xd = x0.to(dev)
         iterate(gd, xd, 2, group)  # warm-up
         t = EventTimer("gpu graph propagate", device=dev)
