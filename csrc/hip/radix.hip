@@ -128,7 +128,7 @@ __device__ __forceinline__ uint64_t os_match(uint32_t d, bool valid) {
 
 // ---------------------------------------------------------------- K1..KP
 template <bool HAS_VALUES>
-__global__ __launch_bounds__(kOsThreads, 4) void radix_onesweep_kernel(
+__global__ __launch_bounds__(kOsThreads, HAS_VALUES ? 2 : 4) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ vout, long long n, int shift, int mode_in, int mode_out,
     const uint32_t* __restrict__ counts, uint64_t* __restrict__ agg, uint64_t* __restrict__ inc,
