@@ -72,11 +72,25 @@ def _newest_header() -> float:
     return max((p.stat().st_mtime for p in INCLUDE.rglob("*.h")), default=0.0)
 
 
+def _local_includes(src: Path) -> list[Path]:
+    """Headers next to a source that it #includes by quoted name (heat_pipe.h
+    is shared by heat_pipe.hip and heat_pipe_tune.hip)."""
+    out = []
+    for line in src.read_text(errors="replace").splitlines():
+        line = line.strip()
+        if line.startswith('#include "') and "/" not in line:
+            h = src.parent / line.split('"')[1]
+            if h.exists():
+                out.append(h)
+    return out
+
+
 def _needs(obj: Path, src: Path, hdr_time: float) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or hdr_time > t
+    local = max((h.stat().st_mtime for h in _local_includes(src)), default=0.0)
+    return src.stat().st_mtime > t or hdr_time > t or local > t
 
 
 def _run(cmd: list[str]) -> None:

@@ -1,0 +1,81 @@
+// Tuning arms of the wave-pipelined heat pass (kernel: heat_pipe.h):
+// rows per phase, prefetch depth, steps per pass, waves per role, wide lanes.
+#include "heat_pipe.h"
+
+// Tuning entry for the wave-pipelined NS-step pass (order 8, FMA): ns 3..6,
+// rows per phase rb, input prefetch depth pd, explicit chunk or tasks per CU.
+namespace {
+template <int NS, int RB>
+int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int pd,
+             int per_cu, hipStream_t s) {
+    switch (pd) {
+        case 1: return launch_pipe_multi<float, 8, NS, true, RB, 1>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, per_cu, s);
+        case 2: return launch_pipe_multi<float, 8, NS, true, RB, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk, per_cu, s);
+        case 11:  // depth 1, non-temporal output stores
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
+                                                                         per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 12:  // depth 1, non-temporal stores, reassociated ("fast") arithmetic
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, 2, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
+                                                                      per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 13:  // the same, registers capped for 4 waves per SIMD
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, 3, RB, 1, true>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl, chunk,
+                                                                      per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 21:  // + two waves per role (seams through LDS)
+            if constexpr (RB == 4)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 2>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 41:  // + four waves per role
+            if constexpr (RB == 4 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 81:  // wide lanes: 8 columns per lane, non-temporal stores
+            if constexpr (RB <= 4 && NS <= 5)
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                               chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
+        case 84:
+            if constexpr (RB == 2 && NS == 4) {
+                if (pd == 83)
+                    return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 1, 8, 3>(p, c, pitch, gy, &g, 1, g, xcfl,
+                                                                                      ycfl, chunk, per_cu, s);
+                return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 1, 8, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                                  chunk, per_cu, s);
+            }
+            return (int)hipErrorInvalidValue;
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+template <int NS>
+int tunep_rb(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int rb, int pd,
+             int per_cu, hipStream_t s) {
+    if (rb == 4) return tunep_pd<NS, 4>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
+    if constexpr (NS <= 4) {
+        if (rb == 2) return tunep_pd<NS, 2>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
+        if (rb == 8) return tunep_pd<NS, 8>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
+    }
+    return (int)hipErrorInvalidValue;
+}
+}  // namespace
+
+CME_EXPORT int cme_heat_pipe_tune(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
+                                  float xcfl, float ycfl, int chunk, int rb, int ns, int pd, int per_cu,
+                                  void* stream) {
+    hipStream_t s = as_stream(stream);
+    const Region g{xb, xe, yb, ye};
+    switch (ns) {
+        case 3: return tunep_rb<3>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, per_cu, s);
+        case 4: return tunep_rb<4>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, per_cu, s);
+        case 5: return tunep_rb<5>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, per_cu, s);
+        case 6: return tunep_rb<6>(prev, curr, pitch, gy, g, xcfl, ycfl, chunk, rb, pd, per_cu, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}

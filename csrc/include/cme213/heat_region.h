@@ -31,10 +31,13 @@ struct StripN {
 };
 
 // Output columns of one strip of the wave-pipelined pass: WPR waves side by
-// side per timestep role (64*WPR lanes, 4 columns each, NS lanes lost per side).
-template <int NS, int WPR>
+// side per timestep role (64*WPR lanes of VW columns). VW = 4: NS lanes lost
+// per side (one lane per step, exact at order 8). VW = 8 (wide lanes): the
+// whole lanes covering the NS*B columns each side loses over NS steps.
+template <int NS, int WPR, int VW = 4, int B = 4>
 struct PipeOut {
-    static constexpr int kOut = (64 * WPR - 2 * NS) * 4;
+    static constexpr int kMargin = VW == 4 ? NS : (NS * B + VW - 1) / VW;
+    static constexpr int kOut = (64 * WPR - 2 * kMargin) * VW;
 };
 
 // Fused-schedule gate of the pipelined pass: workgroups of regions

@@ -56,6 +56,36 @@ __device__ __forceinline__ void store4(T* p, const V4<T>& r) {
     }
 }
 
+// N (a multiple of 4) consecutive elements per lane, moved as N/4 16-B (fp32)
+// pieces: the wide-lane pipelined heat pass keeps 8 columns per lane.
+template <typename T, int N>
+struct alignas(16) VecN {
+    static_assert(N % 4 == 0, "VecN: multiple of 4 elements");
+    T v[N];
+    __device__ __forceinline__ T& operator[](int i) { return v[i]; }
+    __device__ __forceinline__ const T& operator[](int i) const { return v[i]; }
+};
+
+template <int N, typename T>
+__device__ __forceinline__ VecN<T, N> load_n(const T* p) {
+    VecN<T, N> r;
+#pragma unroll
+    for (int h = 0; h < N / 4; ++h) {
+        const V4<T> q = load4(p + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.v[4 * h + j] = q.v[j];
+    }
+    return r;
+}
+
+template <int N, typename T>
+__device__ __forceinline__ V4<T> piece4(const VecN<T, N>& x, int h) {
+    V4<T> q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q.v[j] = x.v[4 * h + j];
+    return q;
+}
+
 // Whole-vector lane shifts: lane i receives lane i-1 (shr) / i+1 (shl); the
 // edge lane (0 for shr, 63 for shl) receives 0.
 template <typename T>

@@ -151,6 +151,36 @@ def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("region", [(9, 1400, 6, 690), (130, 131, 5, 200), (4, 484, 4, 100), (600, 1100, 33, 47),
+                                    (4, 1504, 4, 704), (12, 20, 4, 704)])
+def test_gpu_pipe_wide_lanes_bitwise(gpu, region):
+    """Wide lanes (8 columns per lane, strips on 8-column boundaries, so edge
+    lanes straddle region starts like x = 4, 9, 12): equal to ns single FMA
+    steps for ns 3-5, 2 and 4 rows per phase, short explicit chunks and the
+    default chunk rule, on regions narrower than, equal to and wider than one
+    strip, up to the whole interior."""
+    from cme213x import _ext
+    from cme213x.ops.stencil import heat_run
+    p = SimParams(nx=1500, ny=700, order=8)
+    c = _rand_grid(p, torch.float32, seed=6)
+    g = _rand_grid(p, torch.float32, gpu, seed=6)
+    xb, xe, yb, ye = region
+    oracle = {}
+    for ns in (3, 4, 5):
+        ca, cb = c.buf[0].clone(), c.buf[0].clone()
+        oracle[ns] = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, ns, "fma").clone()
+    s = _ext.stream_ptr(g.buf[0].device)
+    arms = [(ns, rb, pc, ch) for ns in (3, 4) for rb in (2, 4) for pc, ch in ((2, 0), (0, 10), (0, 0))]
+    arms += [(5, 4, 0, 0), (5, 4, 0, 12)]
+    for ns, rb, pc, ch in arms:
+        out = g.buf[0].clone()
+        _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, xb, xe, yb, ye,
+                      g.xcfl, g.ycfl, ch, rb, ns, 81, pc, s)
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), oracle[ns]), (ns, rb, pc, ch)
+
+
+@pytest.mark.gpu
 def test_gpu_pipe_gated_regions(gpu):
     """The fused-schedule entry (cme_heat_pipe_gated_f32): deep interior plus
     gated border strips in one launch, gate already open, equals the plain
