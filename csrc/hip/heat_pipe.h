@@ -52,7 +52,14 @@ __device__ __forceinline__ float uniform_f(float v) {
 // are the centre rows of phase q+1 (needs RB == B), which the neighbour wave
 // reads back as the `old` operand of its DPP shifts (the lane with no DPP
 // source keeps it). Three edge buffers, one barrier per phase.
-template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR = 1, int VW = 4>
+//
+// LX (x-neighbours from LDS): roles 1..NS-1 read the B edge columns of the
+// lanes on either side of their centre rows back from the ring (two 16-B LDS
+// reads per row) instead of shifting them across lanes with 2B DPP moves on
+// the VALU; the centre rows arrived B/RB phases earlier, so the ring keeps
+// 2 + B/RB slots. Role 0 (rows from HBM) keeps the DPP shifts.
+template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR = 1, int VW = 4,
+          bool LX = false>
 struct PipeN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
@@ -63,8 +70,15 @@ struct PipeN {
     static_assert(WPR == 1 || (RB == B && sizeof(T) == 4 && VW == 4),
                   "pipe: WPR > 1 needs RB == B (order 8, RB 4), fp32, 4 columns per lane");
     static_assert(VW == 4 || (VW == 8 && sizeof(T) == 4 && B <= VW), "pipe: wide lanes are fp32, 8 columns");
+    static_assert(!LX || (WPR == 1 && B % RB == 0), "pipe: LDS x-neighbours need one wave per role, RB | B");
+    static constexpr int NSLOT = LX ? 2 + B / RB : 2;  // ring slots per role hand-off
+    // FMA: 0 exact, 1 FMA-contracted (the reference's nvcc -fmad code), 2 / 3
+    // reassociated ("fast"; 3 capped at 4 waves/SIMD), 4 FMA-contracted with
+    // the chains of the lane's VW points interleaved term by term (bitwise 1)
+    static constexpr bool kFast = FMA == 2 || FMA == 3;
+    static constexpr bool kTermMajor = FMA == 4;
     using VT = VecN<T, VW>;
-    using Ring = V4<T>[2][RB][NH][LW];
+    using Ring = V4<T>[NSLOT][RB][NH][LW];
     using Edge = V4<T>[3][RB][WPR][2];
 
     VT w[NW];           // window of step-k rows (k = this wave's role); slot j = row r0 - (k+1)B + j
@@ -74,10 +88,11 @@ struct PipeN {
     const T* src;
     T* dst;
     int pitch, gy, xbase, lane, sub, glane, e3;
+    int gl_l, gl_r;  // LX: the neighbour lanes (clamped into the strip; edge lanes are margin lanes)
     bool out_lane, full_vec;
     int y0, y1, xb, xe, xb1, xe1, yb1, ye1;
     T xcfl, ycfl;
-    HeatFast<ORDER, T> fc;  // FMA >= 2 (3: capped at 4 waves/SIMD): folded weights, wave-uniform
+    HeatFast<ORDER, T> fc;  // kFast: folded weights, wave-uniform
     int r0, q;
 
     __device__ __forceinline__ const T* row_ptr(int r) const {
@@ -90,11 +105,18 @@ struct PipeN {
     // seam of WPR > 1 takes the neighbour wave's value from `ev`). VW = 8
     // moves 2B = 8 values per 8 points instead of per 4, and pairs more of the
     // x operands inside one lane for the packed FMAs.
-    template <bool MASK>
-    __device__ __forceinline__ VT upd(int s_lo, int row, const V4<T>& ev) const {
+    template <bool MASK, bool FROM_LDS = false>
+    __device__ __forceinline__ VT upd(int s_lo, int row, const V4<T>& ev, const V4<T>& xl = V4<T>{},
+                                      const V4<T>& xr = V4<T>{}) const {
         const VT c = w[(s_lo + B) % NW];
         T rowv[VW + 2 * B];
-        if constexpr (WPR == 1) {
+        if constexpr (FROM_LDS) {  // the left lane's last B columns, the right lane's first B
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                rowv[k] = xl[4 - B + k];
+                rowv[B + VW + k] = xr[k];
+            }
+        } else if constexpr (WPR == 1) {
 #pragma unroll
             for (int k = 0; k < B; ++k) {
                 rowv[k] = dpp_shift<kDppWaveShr1>(c[VW - B + k]);
@@ -112,6 +134,35 @@ struct PipeN {
         bool row_in = true;
         if constexpr (MASK) row_in = row >= yb1 && row < ye1;
         VT o;
+        if constexpr (kTermMajor) {
+            T cc[VW], xm[B][VW], xp[B][VW], ym[B][VW], yp[B][VW], dx[VW], dy[VW];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) {
+                cc[j] = c[j];
+#pragma unroll
+                for (int k = 0; k < B; ++k) {
+                    xm[k][j] = rowv[B + j - (k + 1)];
+                    xp[k][j] = rowv[B + j + (k + 1)];
+                    ym[k][j] = w[(s_lo + B - (k + 1)) % NW][j];
+                    yp[k][j] = w[(s_lo + B + (k + 1)) % NW][j];
+                }
+            }
+            heat_d2_fma_n<ORDER, VW>(dx, cc, xm, xp);
+            heat_d2_fma_n<ORDER, VW>(dy, cc, ym, yp);
+#pragma unroll
+            for (int j = 0; j < VW; ++j) dx[j] = fmaT<T>(xcfl, dx[j], cc[j]);
+#pragma unroll
+            for (int j = 0; j < VW; ++j) {
+                const T u = fmaT<T>(ycfl, dy[j], dx[j]);
+                if constexpr (MASK) {
+                    const int x = xbase + j;
+                    o[j] = (row_in && x >= xb1 && x < xe1) ? u : c[j];
+                } else {
+                    o[j] = u;
+                }
+            }
+            return o;
+        }
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
             T xm[B], xp[B], ym[B], yp[B];
@@ -123,7 +174,7 @@ struct PipeN {
                 yp[k] = w[(s_lo + B + (k + 1)) % NW][j];
             }
             T u;
-            if constexpr (FMA >= 2)
+            if constexpr (kFast)
                 u = heat_update_fast<ORDER>(c[j], xm, xp, ym, yp, fc);
             else
                 u = heat_update_sel<ORDER, FMA != 0>(c[j], xm, xp, ym, yp, xcfl, ycfl);
@@ -157,7 +208,8 @@ struct PipeN {
         if (r0 - (NS - 1) * B >= y1) return false;
         constexpr int S = (PH * RB) % NW;
         constexpr int ST = K + 1;  // the timestep this role computes
-        const int par = q & 1;
+        const int par = q % NSLOT;
+        const int cslot = (q + NSLOT - B / RB) % NSLOT;  // LX: slot of this phase's centre rows
         if constexpr (K == 0) {
             constexpr int F = PH % PD;
 #pragma unroll
@@ -195,12 +247,22 @@ struct PipeN {
             const int row = r0 - (ST - 1) * B + i;
             if constexpr (ST < NS) {
                 if (row >= y0 - (NS - ST) * B && row < y1 + (NS - ST) * B) {
-                    const VT o = upd<CHECK>((S + i) % NW, row, ev[i]);
+                    VT o;
+                    if constexpr (LX && K > 0)
+                        o = upd<CHECK, true>((S + i) % NW, row, ev[i], ring[K - 1][cslot][i][NH - 1][gl_l],
+                                             ring[K - 1][cslot][i][0][gl_r]);
+                    else
+                        o = upd<CHECK>((S + i) % NW, row, ev[i]);
 #pragma unroll
                     for (int h = 0; h < NH; ++h) ring[K][par][i][h][glane] = piece4(o, h);
                 }
             } else if (row >= y0 && row < y1) {
-                const VT o = upd<false>((S + i) % NW, row, ev[i]);
+                VT o;
+                if constexpr (LX && K > 0)
+                    o = upd<false, true>((S + i) % NW, row, ev[i], ring[K - 1][cslot][i][NH - 1][gl_l],
+                                         ring[K - 1][cslot][i][0][gl_r]);
+                else
+                    o = upd<false>((S + i) % NW, row, ev[i]);
                 T* d = dst + (size_t)row * pitch;
                 if constexpr (!CHECK) {
                     if (out_lane) store_out(d, o);
@@ -266,16 +328,20 @@ struct PipeN {
     }
 };
 
-template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR, int VW>
-__device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][VW / 4][64 * WPR], V4<T> (*edge)[3][RB][WPR][2],
+template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR, int VW, bool LX,
+          int NSLOT>
+__device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * WPR], V4<T> (*edge)[3][RB][WPR][2],
                                           int k, int sub, const T* src, T* dst, int pitch, int gy, int xbase,
                                           int lane, bool out_lane, bool full_vec, int y0, int y1, int xb, int xe,
                                           int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl) {
-    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR, VW> st;
+    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR, VW, LX> st;
+    static_assert(decltype(st)::NSLOT == NSLOT, "pipe: ring slots");
     st.ring = ring;
     st.edge = edge;
     st.sub = sub;
     st.glane = sub * 64 + lane;
+    st.gl_l = st.glane > 0 ? st.glane - 1 : 0;
+    st.gl_r = st.glane < 64 * WPR - 1 ? st.glane + 1 : 64 * WPR - 1;
     st.src = src;
     st.dst = dst;
     st.pitch = pitch;
@@ -294,7 +360,7 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][VW / 4][64 * WPR]
     st.ye1 = ye1;
     st.xcfl = xcfl;
     st.ycfl = ycfl;
-    if constexpr (FMA >= 2) {
+    if constexpr (FMA == 2 || FMA == 3) {
         const HeatFast<ORDER, T> f = heat_fast_coefs<ORDER>(xcfl, ycfl);
         st.fc.c0 = uniform_f(f.c0);
 #pragma unroll
@@ -311,12 +377,13 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[2][RB][VW / 4][64 * WPR]
 // columns lie wholly inside or wholly outside the grid (the edge lanes' loads
 // are clamped into the row).
 template <typename T, int ORDER, int RB, int NS, int FMA, int PD = 1, bool NT = false, int WPR = 1, int VW = 4,
-          int OCC = (FMA == 3 ? 4 : 0)>
+          int OCC = (FMA == 3 ? 4 : 0), bool LX = false>
 __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void heat_pipe_kernel(
     const T* __restrict__ prev, T* __restrict__ curr, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1,
     int ye1, T xcfl, T ycfl, PipeGate gate) {
     static_assert(NS >= 2 && NS <= 6, "pipe: 2..6 steps per pass");
-    __shared__ V4<T> ring[NS - 1][2][RB][VW / 4][64 * WPR];
+    constexpr int NSLOT = PipeN<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX>::NSLOT;
+    __shared__ V4<T> ring[NS - 1][NSLOT][RB][VW / 4][64 * WPR];
     __shared__ V4<T> edge[WPR > 1 ? NS : 1][3][RB][WPR][2];
     constexpr int B = HeatOrder<ORDER>::B;
     using G = PipeOut<NS, WPR, VW, B>;
@@ -368,11 +435,11 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
     const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
                         (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
     if (inside)
-        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
+        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
                                                                  gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
                                                                  xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
     else
-        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
+        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
                                                                 gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
                                                                 xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
 }
@@ -443,14 +510,14 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
 }
 
 template <typename T, int ORDER, int NS, int FMA, int RB, int PD = 1, bool NT = false, int WPR = 1, int VW = 4,
-          int OCC = (FMA == 3 ? 4 : 0)>
+          int OCC = (FMA == 3 ? 4 : 0), bool LX = false>
 int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* gs, int n, Region g1, T xcfl, T ycfl,
                       int chunk_hint, int per_cu, hipStream_t s, PipeGate gate = PipeGate{}) {
     if (n < 1 || n > kMaxS2Regions) return (int)hipErrorInvalidValue;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
     static const long resident = [] {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC, LX>,
                                                          NS * WPR * 64, 0) != hipSuccess || per_cu < 1)
             per_cu = 1;
         return (long)per_cu * device_cu_count();
@@ -482,7 +549,7 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         const long gated = tasks - (gate.from > 0 ? R.wave_end[gate.from - 1] : 0);
         if (2 * gated > resident) return (int)hipErrorInvalidConfiguration;
     }
-    hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC>), dim3(tasks), dim3(NS * WPR * 64), 0, s,
+    hipLaunchKernelGGL((heat_pipe_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC, LX>), dim3(tasks), dim3(NS * WPR * 64), 0, s,
                        prev, curr, pitch, gy, R, g1.xb, g1.xe, g1.yb, g1.ye, xcfl, ycfl, gate);
     CME_LAUNCH_STATUS();
 }

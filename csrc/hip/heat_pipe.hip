@@ -3,11 +3,13 @@
 
 // Production entry: NS (3, 4) timesteps in one pass, like cme_heat_stepn_f32
 // (intermediate steps over `ext`, the last writes `out`, nout <= 4 regions).
-// fp32: wide lanes (8 columns per lane), RB = 2 rows per phase (156 VGPRs,
-// 3 waves per SIMD), one phase of input loads in flight, non-temporal output
-// stores: 0.1311 vs 0.1417 ms/step for the round-2 4-column pass (RB 4) on
-// the bench's 16384^2 field (benchmarks/tune_heat_pipe.py,
-// profiles/heat_pipe_wide_r3.md). CME_PIPE_VW=4 selects the 4-column pass.
+// fp32 order 8: wide lanes (8 columns per lane), RB = 2 rows per phase (156
+// VGPRs, 3 waves per SIMD), the FMA chains of a lane's 8 points interleaved,
+// one phase of input loads in flight, non-temporal output stores: 0.1308 vs
+// 0.1417 ms/step for the round-2 4-column pass (RB 4) on the bench's 16384^2
+// field (benchmarks/tune_heat_pipe.py, profiles/heat_pipe_wide_r3.md).
+// Orders 2 / 4 keep 4 columns per lane (faster on the 4000^2 rows there).
+// CME_PIPE_VW=4 selects the 4-column pass for order 8 too.
 namespace {
 int pipe_vw() {
     static const int v = [] {
@@ -20,18 +22,19 @@ int pipe_vw() {
 template <int ORDER, bool FMA>
 int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, float xcfl,
             float ycfl, int chunk, hipStream_t s, PipeGate gate) {
-    const bool wide = pipe_vw() == 8;
+    constexpr int FW = FMA ? 4 : 0;  // wide lanes: term-major FMA chains (bitwise = FMA)
+    if constexpr (ORDER == 8) {
+        if (pipe_vw() == 8) {
+            switch (ns) {
+                case 3: return launch_pipe_multi<float, ORDER, 3, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+                case 4: return launch_pipe_multi<float, ORDER, 4, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+                default: return (int)hipErrorInvalidValue;
+            }
+        }
+    }
     switch (ns) {
-        case 3:
-            return wide ? launch_pipe_multi<float, ORDER, 3, FMA, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl,
-                                                                                     ycfl, chunk, 0, s, gate)
-                        : launch_pipe_multi<float, ORDER, 3, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl,
-                                                                             chunk, 0, s, gate);
-        case 4:
-            return wide ? launch_pipe_multi<float, ORDER, 4, FMA, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl,
-                                                                                     ycfl, chunk, 0, s, gate)
-                        : launch_pipe_multi<float, ORDER, 4, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl,
-                                                                             chunk, 0, s, gate);
+        case 3: return launch_pipe_multi<float, ORDER, 3, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+        case 4: return launch_pipe_multi<float, ORDER, 4, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -144,6 +147,6 @@ CME_EXPORT int cme_heat_pipe_gated_f64(const double* prev, double* curr, int pit
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(heat_pipe3_fma_f32_o8, 192, heat_pipe_kernel<float, 8, 4, 3, true, 1, true>);
 CME_REGISTER_KERNEL(heat_pipe4_fma_f32_o8, 256, heat_pipe_kernel<float, 8, 4, 4, true, 1, true>);
-CME_REGISTER_KERNEL(heat_pipe3w_fma_f32_o8, 192, heat_pipe_kernel<float, 8, 2, 3, true, 1, true, 1, 8>);
-CME_REGISTER_KERNEL(heat_pipe4w_fma_f32_o8, 256, heat_pipe_kernel<float, 8, 2, 4, true, 1, true, 1, 8>);
+CME_REGISTER_KERNEL(heat_pipe3w_fma_f32_o8, 192, heat_pipe_kernel<float, 8, 2, 3, 4, 1, true, 1, 8>);
+CME_REGISTER_KERNEL(heat_pipe4w_fma_f32_o8, 256, heat_pipe_kernel<float, 8, 2, 4, 4, 1, true, 1, 8>);
 CME_REGISTER_KERNEL(heat_pipe4w_f32_o8, 256, heat_pipe_kernel<float, 8, 2, 4, false, 1, true, 1, 8>);

@@ -41,6 +41,16 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, true, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                                chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 85:  // wide lanes, FMA chains interleaved across the lane's points (bitwise = 81)
+            if constexpr (RB <= 4 && NS <= 5)
+                return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 86:  // wide lanes, term-major FMA chains, roles 1.. read x-neighbours from the LDS ring
+            if constexpr (RB <= 4 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8, 0, true>(p, c, pitch, gy, &g, 1, g, xcfl,
+                                                                                     ycfl, chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
         case 84:
             if constexpr (RB == 2 && NS == 4) {

@@ -92,6 +92,32 @@ CME_HD T heat_d2_fma(T c, const T* m, const T* p) {
     }
 }
 
+// heat_d2_fma over N points at once, term-major: every FMA of the chain is
+// issued for all N points before the next, so the N independent chains
+// interleave (a chain-major order leaves each packed FMA waiting on the one
+// before it). Per point the same operations in the same order: bitwise equal
+// to heat_d2_fma. m[k][j] / p[k][j] = u(x_j -/+ (k+1)).
+template <int ORDER, int N, typename T>
+CME_HD void heat_d2_fma_n(T* out, const T* c, const T (*m)[N], const T (*p)[N]) {
+    if constexpr (ORDER == 2) {
+        for (int j = 0; j < N; ++j) out[j] = fmaT<T>(T(-2), c[j], p[0][j] + m[0][j]);
+    } else if constexpr (ORDER == 4) {
+        for (int j = 0; j < N; ++j) out[j] = -p[1][j];
+        for (int j = 0; j < N; ++j) out[j] = fmaT<T>(T(16), p[0][j], out[j]);
+        for (int j = 0; j < N; ++j) out[j] = fmaT<T>(T(-30), c[j], out[j]);
+        for (int j = 0; j < N; ++j) out[j] = fmaT<T>(T(16), m[0][j], out[j]);
+        for (int j = 0; j < N; ++j) out[j] = out[j] - m[1][j];
+    } else {
+        const T w[4] = {T(8064), T(-1008), T(128), T(-9)};
+        for (int j = 0; j < N; ++j) out[j] = T(-9) * p[3][j];
+        for (int k = 2; k >= 0; --k)
+            for (int j = 0; j < N; ++j) out[j] = fmaT<T>(w[k], p[k][j], out[j]);
+        for (int j = 0; j < N; ++j) out[j] = fmaT<T>(T(-14350), c[j], out[j]);
+        for (int k = 0; k < 4; ++k)
+            for (int j = 0; j < N; ++j) out[j] = fmaT<T>(w[k], m[k][j], out[j]);
+    }
+}
+
 template <int ORDER, typename T>
 CME_HD T heat_update_fma(T c, const T* xm, const T* xp, const T* ym, const T* yp, T xcfl, T ycfl) {
     const T dx = heat_d2_fma<ORDER>(c, xm, xp);

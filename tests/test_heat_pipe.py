@@ -156,9 +156,11 @@ def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
 def test_gpu_pipe_wide_lanes_bitwise(gpu, region):
     """Wide lanes (8 columns per lane, strips on 8-column boundaries, so edge
     lanes straddle region starts like x = 4, 9, 12): equal to ns single FMA
-    steps for ns 3-5, 2 and 4 rows per phase, short explicit chunks and the
-    default chunk rule, on regions narrower than, equal to and wider than one
-    strip, up to the whole interior."""
+    steps for ns 3-5, 2 and 4 rows per phase, chain-major (81) and term-major
+    (85, production) FMA order, x-neighbours from the LDS ring (86), register
+    caps (83/84), short explicit chunks
+    and the default chunk rule, on regions narrower than, equal to and wider
+    than one strip, up to the whole interior."""
     from cme213x import _ext
     from cme213x.ops.stencil import heat_run
     p = SimParams(nx=1500, ny=700, order=8)
@@ -170,14 +172,16 @@ def test_gpu_pipe_wide_lanes_bitwise(gpu, region):
         ca, cb = c.buf[0].clone(), c.buf[0].clone()
         oracle[ns] = heat_run(ca, cb, region, 8, c.xcfl, c.ycfl, ns, "fma").clone()
     s = _ext.stream_ptr(g.buf[0].device)
-    arms = [(ns, rb, pc, ch) for ns in (3, 4) for rb in (2, 4) for pc, ch in ((2, 0), (0, 10), (0, 0))]
-    arms += [(5, 4, 0, 0), (5, 4, 0, 12)]
-    for ns, rb, pc, ch in arms:
+    arms = [(ns, rb, pd, pc, ch) for ns in (3, 4) for rb in (2, 4) for pd in (81, 85)
+            for pc, ch in ((2, 0), (0, 10), (0, 0))]
+    arms += [(ns, rb, 86, pc, ch) for ns in (3, 4) for rb in (2, 4) for pc, ch in ((2, 0), (0, 10), (0, 0))]
+    arms += [(5, 4, 81, 0, 0), (5, 4, 85, 0, 12), (4, 2, 83, 0, 0), (4, 2, 84, 0, 0)]
+    for ns, rb, pd, pc, ch in arms:
         out = g.buf[0].clone()
         _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, xb, xe, yb, ye,
-                      g.xcfl, g.ycfl, ch, rb, ns, 81, pc, s)
+                      g.xcfl, g.ycfl, ch, rb, ns, pd, pc, s)
         torch.cuda.synchronize()
-        assert torch.equal(out.cpu(), oracle[ns]), (ns, rb, pc, ch)
+        assert torch.equal(out.cpu(), oracle[ns]), (ns, rb, pd, pc, ch)
 
 
 @pytest.mark.gpu
