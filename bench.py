@@ -348,9 +348,9 @@ def main() -> int:
                             f"{'pipe' if args.kernel == 'pipe' and args.tblock >= 3 else 'stream'}{args.tblock} "
                             f"({args.tblock} steps/pass)") + (" fma" if args.fma else " exact"),
                 "kernel": args.kernel,
-                # pipelined order-8 fp32 pass: 8 columns per lane unless CME_PIPE_VW=4 (heat_pipe.hip)
-                "lane_columns": (4 if os.environ.get("CME_PIPE_VW") == "4" or args.order != 8 else 8)
-                if args.kernel == "pipe" and args.tblock >= 3 else 4,
+                # pipelined fp32 pass: 8 columns per lane at order 8 (CME_PIPE_VW=4 / 8 forces one width)
+                "lane_columns": ({"4": 4, "8": 8}.get(os.environ.get("CME_PIPE_VW", ""), 8 if args.order == 8 else 4)
+                                 if args.kernel == "pipe" and args.tblock >= 3 else 4),
                 "fma": bool(args.fma),
                 "tblock": args.tblock,
                 "device": args.device,

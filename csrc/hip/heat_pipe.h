@@ -53,6 +53,15 @@ __device__ __forceinline__ float uniform_f(float v) {
 // reads back as the `old` operand of its DPP shifts (the lane with no DPP
 // source keeps it). Three edge buffers, one barrier per phase.
 //
+// VW = 8 (wide lanes, the order-8 fp32 production pass): each lane holds 8
+// consecutive columns, so the 2B DPP moves of the x-neighbours serve 8 points
+// instead of 4, more packed-FMA operand pairs lie inside one lane, and a strip
+// loses ceil(NS*B/8) lanes per side instead of NS (60 of 64 lanes write at
+// NS = 4). 156 VGPRs at RB = 2: three waves per SIMD. Strips start on
+// 8-column boundaries so no lane straddles the grid edge (profiles/
+// heat_pipe_wide_r3.md). FMA = 4 issues the FMA chains of the lane's points
+// term by term (heat_d2_fma_n): the same operations per point, interleaved.
+//
 // LX (x-neighbours from LDS): roles 1..NS-1 read the B edge columns of the
 // lanes on either side of their centre rows back from the ring (two 16-B LDS
 // reads per row) instead of shifting them across lanes with 2B DPP moves on

@@ -9,12 +9,15 @@
 // 0.1417 ms/step for the round-2 4-column pass (RB 4) on the bench's 16384^2
 // field (benchmarks/tune_heat_pipe.py, profiles/heat_pipe_wide_r3.md).
 // Orders 2 / 4 keep 4 columns per lane (faster on the 4000^2 rows there).
-// CME_PIPE_VW=4 selects the 4-column pass for order 8 too.
+// CME_PIPE_VW=4 / 8 forces one width at every order.
 namespace {
-int pipe_vw() {
+// CME_PIPE_VW: unset = the measured default (8 columns per lane at order 8,
+// 4 at orders 2 / 4), 4 / 8 = that width at every order
+int pipe_vw_env() {
     static const int v = [] {
         const char* e = getenv("CME_PIPE_VW");
-        return (e && atoi(e) == 4) ? 4 : 8;
+        const int x = e ? atoi(e) : 0;
+        return (x == 4 || x == 8) ? x : 0;
     }();
     return v;
 }
@@ -23,13 +26,12 @@ template <int ORDER, bool FMA>
 int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, float xcfl,
             float ycfl, int chunk, hipStream_t s, PipeGate gate) {
     constexpr int FW = FMA ? 4 : 0;  // wide lanes: term-major FMA chains (bitwise = FMA)
-    if constexpr (ORDER == 8) {
-        if (pipe_vw() == 8) {
-            switch (ns) {
-                case 3: return launch_pipe_multi<float, ORDER, 3, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
-                case 4: return launch_pipe_multi<float, ORDER, 4, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
-                default: return (int)hipErrorInvalidValue;
-            }
+    const int env = pipe_vw_env();
+    if (env == 8 || (env == 0 && ORDER == 8)) {
+        switch (ns) {
+            case 3: return launch_pipe_multi<float, ORDER, 3, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+            case 4: return launch_pipe_multi<float, ORDER, 4, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+            default: return (int)hipErrorInvalidValue;
         }
     }
     switch (ns) {
