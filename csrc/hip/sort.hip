@@ -59,15 +59,36 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
     const bool vec = ((uintptr_t)keys & 15u) == 0;  // a tensor view may be 4-B aligned only
-    for (long long i = b0 + threadIdx.x * 4; i < b1; i += kSortThreads * 4) {
+    auto add = [&](uint32_t k) { atomicAdd(&hist[digit_of(rx_key_in(k, mode), shift)], 1u); };
+    // UNR 16-B loads in flight per lane before their LDS atomics (one load at
+    // a time left the kernel waiting on HBM latency: wait-any 0.85 of its
+    // cycles, profiles/sort_r3.md)
+    constexpr int UNR = 4;
+    constexpr long long STEP = (long long)kSortThreads * 4;
+    long long i = b0 + threadIdx.x * 4;
+    if (vec) {
+        for (; i + (UNR - 1) * STEP + 3 < b1; i += UNR * STEP) {
+            uint4 v[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) v[u] = *reinterpret_cast<const uint4*>(keys + i + u * STEP);
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                add(v[u].x);
+                add(v[u].y);
+                add(v[u].z);
+                add(v[u].w);
+            }
+        }
+    }
+    for (; i < b1; i += STEP) {
         if (vec && i + 3 < b1) {
             const uint4 v = *reinterpret_cast<const uint4*>(keys + i);
-            atomicAdd(&hist[digit_of(rx_key_in(v.x, mode), shift)], 1u);
-            atomicAdd(&hist[digit_of(rx_key_in(v.y, mode), shift)], 1u);
-            atomicAdd(&hist[digit_of(rx_key_in(v.z, mode), shift)], 1u);
-            atomicAdd(&hist[digit_of(rx_key_in(v.w, mode), shift)], 1u);
+            add(v.x);
+            add(v.y);
+            add(v.z);
+            add(v.w);
         } else {
-            for (long long j = i; j < b1 && j < i + 4; ++j) atomicAdd(&hist[digit_of(rx_key_in(keys[j], mode), shift)], 1u);
+            for (long long j = i; j < b1 && j < i + 4; ++j) add(keys[j]);
         }
     }
     __syncthreads();
@@ -110,7 +131,10 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return peers;
 }
 
-template <bool HAS_VALUES>
+// ATOMIC_RANK: in-wave ranks through returning LDS atomics issued back to
+// back (else one LDS read-then-write per item); PREFETCH: the next tile's keys
+// load while this tile is reordered and stored (+16 VGPRs)
+template <bool HAS_VALUES, bool ATOMIC_RANK = false, bool PREFETCH = true>
 __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
     const uint32_t* __restrict__ keys_in, uint32_t* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, long long n, long long chunk, int shift, int nblocks,
@@ -131,21 +155,52 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
         s_base[threadIdx.x] = db + prefix[(size_t)threadIdx.x * nblocks + blockIdx.x];
     }
 
-    for (long long t0 = b0; t0 < b1; t0 += kSortTile) {
-        for (int d = threadIdx.x; d < kBins; d += kSortThreads)
-#pragma unroll
-            for (int w = 0; w < kSortWaves; ++w) s_whist[w][d] = 0;
-        __syncthreads();
-        // warp-striped: item k of lane l = key t0 + wid*1024 + k*64 + l (memory order = (k, l))
-        uint32_t key[kItems], val[kItems], rank[kItems];
-        // issue all 16 loads first (the ranking below is LDS-serial)
+    // warp-striped: item k of lane l = key t0 + wid*1024 + k*64 + l (memory order = (k, l));
+    // the next tile's keys are loaded while this tile is reordered and stored
+    uint32_t key[kItems], val[kItems], rank[kItems];
+    auto load_tile = [&](long long t0, uint32_t* kk, uint32_t* vv) {
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
             const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
             const bool ok = i < b1;
-            key[k] = ok ? rx_key_in(keys_in[i], mode_in) : 0xffffffffu;
-            if constexpr (HAS_VALUES) val[k] = ok ? vals_in[i] : 0u;
+            kk[k] = ok ? keys_in[i] : 0xffffffffu;
+            if constexpr (HAS_VALUES) vv[k] = ok ? vals_in[i] : 0u;
         }
+    };
+    if (PREFETCH && b0 < b1) load_tile(b0, key, val);
+    for (long long t0 = b0; t0 < b1; t0 += kSortTile) {
+        for (int d = threadIdx.x; d < kBins; d += kSortThreads)
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) s_whist[w][d] = 0;
+        if (!PREFETCH) load_tile(t0, key, val);
+        __syncthreads();
+        if (mode_in) {
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if (t0 + wid * (kWave * kItems) + k * kWave + lane < b1) key[k] = rx_key_in(key[k], mode_in);
+        }
+        // stable in-wave ranks: the lowest lane of each digit's peer group adds
+        // the group size to the wave's running count with ONE returning LDS
+        // atomic; the atomics of the 16 items issue back to back (one wave's
+        // LDS operations execute in order, so item k sees items < k) and their
+        // old values come back to the peers by a lane shuffle afterwards --
+        // no LDS read-then-write round trip per item
+        if constexpr (!ATOMIC_RANK) {
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
+                const bool ok = i < b1;
+                const uint32_t d = digit_of(key[k], shift);
+                const uint64_t peers = match_digit(d, ok);
+                const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
+                const uint32_t prev = ok ? s_whist[wid][d] : 0u;
+                rank[k] = ok ? prev + below : 0xffffffffu;
+                // the lowest lane of each peer group publishes the new running count
+                if (ok && below == 0) s_whist[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
+                __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its LDS update
+            }
+        } else {
+        uint32_t old[kItems], lead[kItems];
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
             const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
@@ -153,12 +208,17 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
             const uint32_t d = digit_of(key[k], shift);
             const uint64_t peers = match_digit(d, ok);
             const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
-            const uint32_t prev = ok ? s_whist[wid][d] : 0u;
-            rank[k] = prev + below;
-            // the lowest lane of each peer group publishes the new running count
-            if (ok && below == 0) s_whist[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
-            if (!ok) rank[k] = 0xffffffffu;
-            __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its LDS update
+            lead[k] = peers ? (uint32_t)__builtin_ctzll(peers) : (uint32_t)lane;
+            old[k] = 0u;
+            if (ok && below == 0) old[k] = atomicAdd(&s_whist[wid][d], (uint32_t)__builtin_popcountll(peers));
+            rank[k] = ok ? below : 0xffffffffu;
+            __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its atomic
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t prev = (uint32_t)__shfl((int)old[k], (int)lead[k]);
+            if (rank[k] != 0xffffffffu) rank[k] += prev;
+        }
         }
         __syncthreads();
         // per digit: exclusive prefix across waves, tile totals, tile offsets
@@ -194,6 +254,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
             }
         }
         __syncthreads();
+        if (PREFETCH && t0 + kSortTile < b1) load_tile(t0 + kSortTile, key, val);  // in flight during the stores
         const int tile_n = (int)((b1 - t0) < kSortTile ? (b1 - t0) : kSortTile);
         for (int i = threadIdx.x; i < tile_n; i += kSortThreads) {
             const uint32_t k = s_keys[i];
@@ -470,6 +531,19 @@ CME_EXPORT long long cme_radix_ws_bytes(long long n) {
 // [bit0, bit1), ping-ponging through `tmp` so that the last pass writes out;
 // values (optional) likewise. mode: 0 uint32, 1 int32, 2 float32 keys.
 // ws: cme_radix_ws_bytes(n) bytes.
+// downsweep variant (CME_RADIX_DS, for A/B sweeps): bit 0 atomic ranks, bit 1
+// prefetch. Default 2: the four arms are within 3 % of each other at 16M keys
+// (0.348-0.357 ms; the ranking's LDS round trips are not what binds), the
+// prefetch without atomic ranks is best at 48M (0.956 vs 0.981 ms;
+// profiles/sort_r3.md)
+static int radix_ds_variant() {
+    static const int v = [] {
+        const char* e = getenv("CME_RADIX_DS");
+        return e ? (atoi(e) & 3) : 2;
+    }();
+    return v;
+}
+
 CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
                               uint32_t* vtmp, long long n, int mode, int bit0, int bit1, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -496,12 +570,22 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts,
                            mi);
         hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins), dim3(1024), 0, s, counts, nb, totals);
-        if (vin)
-            hipLaunchKernelGGL(radix_downsweep_kernel<true>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
-                               chunk, shift, nb, counts, totals, mi, mo);
-        else
-            hipLaunchKernelGGL(radix_downsweep_kernel<false>, dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n,
-                               chunk, shift, nb, counts, totals, mi, mo);
+        const int dsv = radix_ds_variant();
+#define CME_DS(V, A, P)                                                                                          \
+    hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P>), dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n, \
+                       chunk, shift, nb, counts, totals, mi, mo)
+        if (vin) {
+            if (dsv == 0) CME_DS(true, false, false);
+            else if (dsv == 1) CME_DS(true, true, false);
+            else if (dsv == 2) CME_DS(true, false, true);
+            else CME_DS(true, true, true);
+        } else {
+            if (dsv == 0) CME_DS(false, false, false);
+            else if (dsv == 1) CME_DS(false, true, false);
+            else if (dsv == 2) CME_DS(false, false, true);
+            else CME_DS(false, true, true);
+        }
+#undef CME_DS
         CME_TRY(hipGetLastError());
         ki = ko;
         vi = vo;
