@@ -134,14 +134,20 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
 // ATOMIC_RANK: in-wave ranks through returning LDS atomics issued back to
 // back (else one LDS read-then-write per item); PREFETCH: the next tile's keys
 // load while this tile is reordered and stored (+16 VGPRs)
-template <bool HAS_VALUES, bool ATOMIC_RANK = false, bool PREFETCH = true>
-__global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
+// DS_THREADS: 256 (4096-key tiles) or 512 (8192-key tiles: digit runs of ~32
+// keys, i.e. fewer partially written lines per tile)
+template <bool HAS_VALUES, bool ATOMIC_RANK = false, bool PREFETCH = true, int DS_THREADS = kSortThreads>
+__global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_downsweep_kernel(
     const uint32_t* __restrict__ keys_in, uint32_t* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, long long n, long long chunk, int shift, int nblocks,
     const uint32_t* __restrict__ prefix, const uint32_t* __restrict__ totals, int mode_in, int mode_out) {
-    __shared__ uint32_t s_keys[kSortTile];
-    __shared__ uint32_t s_vals[HAS_VALUES ? kSortTile : 1];
-    __shared__ uint32_t s_whist[kSortWaves][kBins];  // per-wave running counts, then exclusive prefixes
+    constexpr int kWavesD = DS_THREADS / kWave;
+    constexpr int kTileD = DS_THREADS * kItems;
+    static_assert(DS_THREADS >= kBins, "downsweep: one thread per digit");
+    const int tid = threadIdx.x;
+    __shared__ uint32_t s_keys[kTileD];
+    __shared__ uint32_t s_vals[HAS_VALUES ? kTileD : 1];
+    __shared__ uint32_t s_whist[kWavesD][kBins];  // per-wave running counts, then exclusive prefixes
     __shared__ uint32_t s_tile_off[kBins];            // exclusive prefix of tile digit counts
     __shared__ uint32_t s_base[kBins];                // global position of the next key of each digit
     const int lane = lane_id();
@@ -149,47 +155,46 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
     {  // digit bases: scan of the digit totals + this block's row prefix
-        __shared__ uint32_t s_t[kSortWaves];
+        __shared__ uint32_t s_t[kWavesD];
         uint32_t tot;
-        const uint32_t db = block_exclusive_scan<kSortWaves>(totals[threadIdx.x], s_t, tot, OpAdd());
-        s_base[threadIdx.x] = db + prefix[(size_t)threadIdx.x * nblocks + blockIdx.x];
+        const uint32_t db = block_exclusive_scan<kWavesD>(tid < kBins ? totals[tid] : 0u, s_t, tot, OpAdd());
+        if (tid < kBins) s_base[tid] = db + prefix[(size_t)tid * nblocks + blockIdx.x];
     }
 
     // warp-striped: item k of lane l = key t0 + wid*1024 + k*64 + l (memory order = (k, l));
     // the next tile's keys are loaded while this tile is reordered and stored
     uint32_t key[kItems], val[kItems], rank[kItems];
-    auto load_tile = [&](long long t0, uint32_t* kk, uint32_t* vv) {
+    // item k of this lane is a key iff k < nk (items are 64 keys apart)
+    auto items_of = [&](long long t0) {
+        const long long rem = b1 - (t0 + wid * (kWave * kItems) + lane);
+        return rem <= 0 ? 0 : (rem >= (long long)kWave * kItems ? kItems : (int)((rem + kWave - 1) / kWave));
+    };
+    auto load_tile = [&](long long t0) {
+        const long long base = t0 + wid * (kWave * kItems) + lane;
+        const int nk = items_of(t0);
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
-            const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
-            const bool ok = i < b1;
-            kk[k] = ok ? keys_in[i] : 0xffffffffu;
-            if constexpr (HAS_VALUES) vv[k] = ok ? vals_in[i] : 0u;
+            key[k] = k < nk ? keys_in[base + k * kWave] : 0xffffffffu;
+            if constexpr (HAS_VALUES) val[k] = k < nk ? vals_in[base + k * kWave] : 0u;
         }
     };
-    if (PREFETCH && b0 < b1) load_tile(b0, key, val);
-    for (long long t0 = b0; t0 < b1; t0 += kSortTile) {
-        for (int d = threadIdx.x; d < kBins; d += kSortThreads)
+    if (PREFETCH && b0 < b1) load_tile(b0);
+    for (long long t0 = b0; t0 < b1; t0 += kTileD) {
+        for (int d = threadIdx.x; d < kBins; d += DS_THREADS)
 #pragma unroll
-            for (int w = 0; w < kSortWaves; ++w) s_whist[w][d] = 0;
-        if (!PREFETCH) load_tile(t0, key, val);
+            for (int w = 0; w < kWavesD; ++w) s_whist[w][d] = 0;
+        if (!PREFETCH) load_tile(t0);
+        const int nk = items_of(t0);
         __syncthreads();
         if (mode_in) {
 #pragma unroll
             for (int k = 0; k < kItems; ++k)
-                if (t0 + wid * (kWave * kItems) + k * kWave + lane < b1) key[k] = rx_key_in(key[k], mode_in);
+                if (k < nk) key[k] = rx_key_in(key[k], mode_in);
         }
-        // stable in-wave ranks: the lowest lane of each digit's peer group adds
-        // the group size to the wave's running count with ONE returning LDS
-        // atomic; the atomics of the 16 items issue back to back (one wave's
-        // LDS operations execute in order, so item k sees items < k) and their
-        // old values come back to the peers by a lane shuffle afterwards --
-        // no LDS read-then-write round trip per item
         if constexpr (!ATOMIC_RANK) {
 #pragma unroll
             for (int k = 0; k < kItems; ++k) {
-                const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
-                const bool ok = i < b1;
+                const bool ok = k < nk;
                 const uint32_t d = digit_of(key[k], shift);
                 const uint64_t peers = match_digit(d, ok);
                 const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
@@ -200,32 +205,36 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
                 __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its LDS update
             }
         } else {
-        uint32_t old[kItems], lead[kItems];
+            // stable in-wave ranks: the lowest lane of each digit's peer group
+            // adds the group size to the wave's running count with ONE returning
+            // LDS atomic; the atomics of the 16 items issue back to back (one
+            // wave's LDS operations execute in order, so item k sees items < k)
+            // and their old values come back to the peers by a lane shuffle
+            uint32_t old[kItems], lead[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const long long i = t0 + wid * (kWave * kItems) + k * kWave + lane;
-            const bool ok = i < b1;
-            const uint32_t d = digit_of(key[k], shift);
-            const uint64_t peers = match_digit(d, ok);
-            const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
-            lead[k] = peers ? (uint32_t)__builtin_ctzll(peers) : (uint32_t)lane;
-            old[k] = 0u;
-            if (ok && below == 0) old[k] = atomicAdd(&s_whist[wid][d], (uint32_t)__builtin_popcountll(peers));
-            rank[k] = ok ? below : 0xffffffffu;
-            __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its atomic
-        }
+            for (int k = 0; k < kItems; ++k) {
+                const bool ok = k < nk;
+                const uint32_t d = digit_of(key[k], shift);
+                const uint64_t peers = match_digit(d, ok);
+                const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
+                lead[k] = peers ? (uint32_t)__builtin_ctzll(peers) : (uint32_t)lane;
+                old[k] = 0u;
+                if (ok && below == 0) old[k] = atomicAdd(&s_whist[wid][d], (uint32_t)__builtin_popcountll(peers));
+                rank[k] = ok ? below : 0xffffffffu;
+                __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its atomic
+            }
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const uint32_t prev = (uint32_t)__shfl((int)old[k], (int)lead[k]);
-            if (rank[k] != 0xffffffffu) rank[k] += prev;
-        }
+            for (int k = 0; k < kItems; ++k) {
+                const uint32_t prev = (uint32_t)__shfl((int)old[k], (int)lead[k]);
+                if (rank[k] != 0xffffffffu) rank[k] += prev;
+            }
         }
         __syncthreads();
         // per digit: exclusive prefix across waves, tile totals, tile offsets
-        for (int d = threadIdx.x; d < kBins; d += kSortThreads) {
+        for (int d = threadIdx.x; d < kBins; d += DS_THREADS) {
             uint32_t run = 0;
 #pragma unroll
-            for (int w = 0; w < kSortWaves; ++w) {
+            for (int w = 0; w < kWavesD; ++w) {
                 const uint32_t c = s_whist[w][d];
                 s_whist[w][d] = run;
                 run += c;
@@ -235,12 +244,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
         __syncthreads();
         // exclusive scan of the 256 tile counts (one value per thread)
         {
-            __shared__ uint32_t s_tmp[kSortWaves];
+            __shared__ uint32_t s_tmp[kWavesD];
             uint32_t tot;
-            const uint32_t c = s_tile_off[threadIdx.x];
-            const uint32_t ex = block_exclusive_scan<kSortWaves>(c, s_tmp, tot, OpAdd());
+            const uint32_t c = tid < kBins ? s_tile_off[tid] : 0u;
+            const uint32_t ex = block_exclusive_scan<kWavesD>(c, s_tmp, tot, OpAdd());
             __syncthreads();
-            s_tile_off[threadIdx.x] = ex;
+            if (tid < kBins) s_tile_off[tid] = ex;
         }
         __syncthreads();
         // reorder the tile by digit in LDS
@@ -254,9 +263,9 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
             }
         }
         __syncthreads();
-        if (PREFETCH && t0 + kSortTile < b1) load_tile(t0 + kSortTile, key, val);  // in flight during the stores
-        const int tile_n = (int)((b1 - t0) < kSortTile ? (b1 - t0) : kSortTile);
-        for (int i = threadIdx.x; i < tile_n; i += kSortThreads) {
+        if (PREFETCH && t0 + kTileD < b1) load_tile(t0 + kTileD);  // in flight during the stores
+        const int tile_n = (int)((b1 - t0) < kTileD ? (b1 - t0) : kTileD);
+        for (int i = threadIdx.x; i < tile_n; i += DS_THREADS) {
             const uint32_t k = s_keys[i];
             const uint32_t d = digit_of(k, shift);
             const uint32_t g = s_base[d] + (uint32_t)i - s_tile_off[d];
@@ -265,8 +274,8 @@ __global__ __launch_bounds__(kSortThreads) void radix_downsweep_kernel(
         }
         __syncthreads();
         // advance the per-digit bases by this tile's counts
-        {
-            const int d = threadIdx.x;
+        if (tid < kBins) {
+            const int d = tid;
             const uint32_t next = d + 1 < kBins ? s_tile_off[d + 1] : (uint32_t)tile_n;
             s_base[d] += next - s_tile_off[d];
         }
@@ -532,14 +541,14 @@ CME_EXPORT long long cme_radix_ws_bytes(long long n) {
 // values (optional) likewise. mode: 0 uint32, 1 int32, 2 float32 keys.
 // ws: cme_radix_ws_bytes(n) bytes.
 // downsweep variant (CME_RADIX_DS, for A/B sweeps): bit 0 atomic ranks, bit 1
-// prefetch. Default 2: the four arms are within 3 % of each other at 16M keys
+// prefetch, bit 2 8192-key tiles (512 threads). Default 2: the four arms are within 3 % of each other at 16M keys
 // (0.348-0.357 ms; the ranking's LDS round trips are not what binds), the
 // prefetch without atomic ranks is best at 48M (0.956 vs 0.981 ms;
 // profiles/sort_r3.md)
 static int radix_ds_variant() {
     static const int v = [] {
         const char* e = getenv("CME_RADIX_DS");
-        return e ? (atoi(e) & 3) : 2;
+        return e ? (atoi(e) & 7) : 2;
     }();
     return v;
 }
@@ -551,10 +560,13 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     if (bit0 < 0 || bit1 > 32 || bit1 <= bit0 || mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) ||
         (vin && !vtmp) || n >= (1ll << 32))
         return (int)hipErrorInvalidValue;
-    const long long tiles = (n + kSortTile - 1) / kSortTile;
+    const int dsv = radix_ds_variant();
+    const bool wide = (dsv & 4) != 0;  // 8192-key downsweep tiles
+    const long long dtile = wide ? 2 * kSortTile : kSortTile;
+    const long long tiles = (n + dtile - 1) / dtile;
     const int cap = radix_max_blocks();
     int nb = tiles < cap ? (int)tiles : cap;
-    const long long chunk = ((tiles + nb - 1) / nb) * kSortTile;
+    const long long chunk = ((tiles + nb - 1) / nb) * dtile;
     nb = (int)((n + chunk - 1) / chunk);
     uint32_t* counts = (uint32_t*)ws;
     uint32_t* totals = counts + (size_t)nb * kBins;
@@ -570,10 +582,15 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts,
                            mi);
         hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins), dim3(1024), 0, s, counts, nb, totals);
-        const int dsv = radix_ds_variant();
-#define CME_DS(V, A, P)                                                                                          \
-    hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P>), dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi, vo, n, \
-                       chunk, shift, nb, counts, totals, mi, mo)
+#define CME_DS(V, A, P)                                                                                           \
+    do {                                                                                                          \
+        if (wide)                                                                                                 \
+            hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P, 512>), dim3(nb), dim3(512), 0, s, ki, ko, vi, vo, n, \
+                               chunk, shift, nb, counts, totals, mi, mo);                                         \
+        else                                                                                                      \
+            hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P>), dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi,  \
+                               vo, n, chunk, shift, nb, counts, totals, mi, mo);                                  \
+    } while (0)
         if (vin) {
             if (dsv == 0) CME_DS(true, false, false);
             else if (dsv == 1) CME_DS(true, true, false);
