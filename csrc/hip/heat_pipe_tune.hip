@@ -51,6 +51,16 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8, 0, true>(p, c, pitch, gy, &g, 1, g, xcfl,
                                                                                      ycfl, chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 87:  // wide lanes, term-major, prefetch depth 2 (RB 1: 151 VGPRs; RB 2: 175 = 2 waves/SIMD)
+            if constexpr (RB <= 2 && NS == 4)
+                return launch_pipe_multi<float, 8, NS, 4, RB, 2, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 88:  // wide lanes, term-major, RB 1 capped at 4 waves per SIMD (128 VGPRs, 15 spilled)
+            if constexpr (RB == 1 && NS == 4)
+                return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                               chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
         case 84:
             if constexpr (RB == 2 && NS == 4) {
@@ -68,6 +78,9 @@ template <int NS>
 int tunep_rb(const float* p, float* c, int pitch, int gy, Region g, float xcfl, float ycfl, int chunk, int rb, int pd,
              int per_cu, hipStream_t s) {
     if (rb == 4) return tunep_pd<NS, 4>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
+    if constexpr (NS == 4) {
+        if (rb == 1 && pd >= 85) return tunep_pd<NS, 1>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
+    }
     if constexpr (NS <= 4) {
         if (rb == 2) return tunep_pd<NS, 2>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
         if (rb == 8) return tunep_pd<NS, 8>(p, c, pitch, gy, g, xcfl, ycfl, chunk, pd, per_cu, s);
