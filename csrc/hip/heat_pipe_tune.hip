@@ -56,6 +56,11 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, 4, RB, 2, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                             chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 89:  // wide lanes, term-major, RB 1, prefetch depth 3
+            if constexpr (RB == 1 && NS == 4)
+                return launch_pipe_multi<float, 8, NS, 4, RB, 3, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 88:  // wide lanes, term-major, RB 1 capped at 4 waves per SIMD (128 VGPRs, 15 spilled)
             if constexpr (RB == 1 && NS == 4)
                 return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
