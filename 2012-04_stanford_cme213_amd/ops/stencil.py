@@ -42,17 +42,20 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fast_f64", "ppiiiiiidd")
 
 VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
             "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,
-            "stream4_fma": 10, "pipe3": 11, "pipe3_fma": 12, "pipe4": 13, "pipe4_fma": 14}
+            "stream4_fma": 10, "pipe3": 11, "pipe3_fma": 12, "pipe4": 13, "pipe4_fma": 14, "pipe5": 15,
+            "pipe5_fma": 16, "pipe6": 17, "pipe6_fma": 18}
 # variants that advance more than one timestep per launch (multi-step drivers
 # only); stream4 (4 steps per HBM pass) is fp32 only, stream3 takes fp32 and
 # fp64 (one row per register block for doubles); pipeN = the wave-pipelined
-# N-step pass (csrc/hip/heat_pipe.hip), fp32 and fp64
+# N-step pass (csrc/hip/heat_pipe.hip), fp32 and fp64 (pipe5 / pipe6: fp32, for
+# the HBM-bound low orders)
 MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma", "pipe3", "pipe3_fma",
-             "pipe4", "pipe4_fma"}
-FP32_ONLY = {"stream4", "stream4_fma"}
+             "pipe4", "pipe4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma"}
+FP32_ONLY = {"stream4", "stream4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
-FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma"}
+FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma",
+                "pipe5_fma", "pipe6_fma"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:

@@ -805,15 +805,18 @@ int launch_heat(int variant, const T* prev, T* curr, int pitch, int gy, Region g
         } else {
             return (int)hipErrorInvalidValue;
         }
-    } else if (variant >= 11 && variant <= 14) {
-        // wave-pipelined NS = 3 (11 exact, 12 FMA) / 4 (13, 14) steps per pass
+    } else if (variant >= 11 && variant <= 18) {
+        // wave-pipelined NS = 3 (11 exact, 12 FMA) / 4 (13, 14) / 5 (15, 16) /
+        // 6 (17, 18, fp32) steps per pass
         const int r[4] = {g.xb, g.xe, g.yb, g.ye};
+        const int ns = (variant - 11) / 2 + 3;
         if constexpr (sizeof(T) == 4)
-            return cme_heat_pipe_f32(prev, curr, pitch, gy, r, 1, r, ORDER, variant <= 12 ? 3 : 4, xcfl, ycfl,
-                                     chunk_hint, (variant & 1) ? 0 : 1, s);
+            return cme_heat_pipe_f32(prev, curr, pitch, gy, r, 1, r, ORDER, ns, xcfl, ycfl, chunk_hint,
+                                     (variant & 1) ? 0 : 1, s);
         else
-            return cme_heat_pipe_f64(prev, curr, pitch, gy, r, 1, r, ORDER, variant <= 12 ? 3 : 4, xcfl, ycfl,
-                                     chunk_hint, (variant & 1) ? 0 : 1, s);
+            return ns > 4 ? (int)hipErrorInvalidValue
+                          : cme_heat_pipe_f64(prev, curr, pitch, gy, r, 1, r, ORDER, ns, xcfl, ycfl, chunk_hint,
+                                              (variant & 1) ? 0 : 1, s);
     } else if (variant == 3) {
         // LDS tile without the +1 pad (bank-conflict study arm).
         constexpr int TY = 32;
@@ -981,7 +984,7 @@ CME_EXPORT int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, i
 // steps), 5 stream2 FMA (TWO steps), 6 stream FMA, 7 / 8 stream3 exact / FMA
 // (THREE steps, fp32), 9 / 10 stream4 exact / FMA (FOUR steps, fp32),
 // 11 / 12 pipe3 exact / FMA, 13 / 14 pipe4 exact / FMA (wave-pipelined, fp32
-// and fp64)
+// and fp64), 15 / 16 pipe5, 17 / 18 pipe6 (fp32: HBM-bound low orders)
 CME_EXPORT int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int variant, float xcfl, float ycfl, int chunk, void* stream) {
     return dispatch_heat<float>(order, variant, prev, curr, pitch, gy, Region{xb, xe, yb, ye}, xcfl, ycfl, chunk,
@@ -1006,9 +1009,9 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int cur = 0;
     T* bufs[2] = {a, b};
     int i = 0;
-    if (variant >= 7 && variant <= 14) {
-        if (sizeof(T) != 4 && (variant == 9 || variant == 10)) return (int)hipErrorInvalidValue;
-        const int ns = (variant <= 8 || variant == 11 || variant == 12) ? 3 : 4;
+    if (variant >= 7 && variant <= 18) {
+        if (sizeof(T) != 4 && (variant == 9 || variant == 10 || variant >= 15)) return (int)hipErrorInvalidValue;
+        const int ns = variant >= 11 ? (variant - 11) / 2 + 3 : (variant <= 8 ? 3 : 4);
         for (; i + ns <= iters; i += ns) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
             if (rc) return rc;

@@ -31,12 +31,17 @@ int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n
         switch (ns) {
             case 3: return launch_pipe_multi<float, ORDER, 3, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
             case 4: return launch_pipe_multi<float, ORDER, 4, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+            case 5: return launch_pipe_multi<float, ORDER, 5, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+            case 6: return launch_pipe_multi<float, ORDER, 6, FW, 2, 1, true, 1, 8>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
             default: return (int)hipErrorInvalidValue;
         }
     }
     switch (ns) {
         case 3: return launch_pipe_multi<float, ORDER, 3, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         case 4: return launch_pipe_multi<float, ORDER, 4, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+        // 5 / 6 steps per pass: orders 2 / 4 are HBM-bound at 4 (profiles/heat_pipe_wide_r3.md)
+        case 5: return launch_pipe_multi<float, ORDER, 5, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+        case 6: return launch_pipe_multi<float, ORDER, 6, FMA, 4, 1, true>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         default: return (int)hipErrorInvalidValue;
     }
 }

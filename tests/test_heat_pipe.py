@@ -31,6 +31,35 @@ def test_pipe_variants_are_multistep_any_dtype():
     assert "pipe4_fma" in FMA_VARIANTS and "pipe4" not in FMA_VARIANTS
 
 
+def test_pipe56_variants_fp32_only():
+    from cme213x.ops.stencil import FMA_VARIANTS, FP32_ONLY, MULTISTEP, heat_run
+    for v in ("pipe5", "pipe5_fma", "pipe6", "pipe6_fma"):
+        assert v in MULTISTEP and v in FP32_ONLY
+    assert {"pipe5_fma", "pipe6_fma"} <= FMA_VARIANTS
+    p = SimParams(nx=20, ny=20, order=2)
+    g = HeatGrid(p, torch.float64)
+    with pytest.raises(ValueError):
+        heat_run(g.buf[0], g.buf[1], g.interior, 2, g.xcfl, g.ycfl, 6, "pipe6")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4, 8])
+@pytest.mark.parametrize("ns", [5, 6])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("iters", [5, 6, 13])
+def test_gpu_pipe56_temporal_blocking_bitwise(gpu, order, ns, fma, iters):
+    """Five and six steps per pass (fp32; the HBM-bound low orders), remainders
+    through two-step and single passes: bitwise equal to single steps."""
+    p = SimParams(nx=517, ny=263, order=order)
+    c = _rand_grid(p, torch.float32)
+    g = _rand_grid(p, torch.float32, gpu)
+    c.run(iters, "fma" if fma else "naive")
+    g.run(iters, f"pipe{ns}" + ("_fma" if fma else ""))
+    torch.cuda.synchronize()
+    d = ulp_distance(c.state(), g.state())
+    assert int(d.max()) == 0, f"max ulp {int(d.max())}"
+
+
 def test_pipe_kernel_name_checked():
     from cme213x.ops.stencil import heat_stepn
     p = SimParams(nx=20, ny=20, order=8)
