@@ -84,6 +84,51 @@ def to_csr_aligned(a: CSR) -> CSRAligned:
 
 
 @dataclass
+class CSRColBlocked:
+    """Aligned CSR split into column blocks, multiplied block after block
+    (y = A_0 x_0, then y += A_k x_k). Each block's slice of ``x`` is small
+    enough (<= ``block_bytes``, half of one XCD's 4 MB L2) to stay L2-resident
+    while the block's column / value stream passes through non-temporally, so
+    the random gathers hit L2 instead of the Infinity Cache (the x-caching
+    idea of ``refs/Baskaran IBM 2009.pdf`` pp.4-8, by column range). The
+    row sums are taken per block, then added: the same value up to fp32
+    reassociation (within the tolerance of the reference's checks)."""
+    nrows: int
+    ncols: int
+    col0: tuple  # first column of each block
+    blocks: tuple  # CSRAligned per block, column indices relative to col0
+
+    @property
+    def nnz(self) -> int:
+        return sum(b.nnz for b in self.blocks)
+
+    def to(self, device) -> "CSRColBlocked":
+        return CSRColBlocked(self.nrows, self.ncols, self.col0, tuple(b.to(device) for b in self.blocks))
+
+
+def to_csr_colblocked(a: CSR, block_bytes: int = 2 << 20) -> CSRColBlocked:
+    """Split ``a`` into ceil(4 * ncols / block_bytes) column blocks of equal
+    width (aligned CSR each; column indices made block-relative)."""
+    nb = max(1, -(-4 * a.ncols // block_bytes))
+    width = -(-a.ncols // nb)
+    rp = a.rp.cpu().long()
+    col = a.col.cpu().long()
+    val = a.val.cpu()
+    rows = torch.repeat_interleave(torch.arange(a.nrows), torch.diff(rp))
+    blk = col // width
+    blocks, col0 = [], []
+    for k in range(nb):
+        sel = blk == k
+        r, c, v = rows[sel], col[sel] - k * width, val[sel]
+        brp = torch.zeros(a.nrows + 1, dtype=torch.long)
+        brp[1:] = torch.cumsum(torch.bincount(r, minlength=a.nrows), 0)
+        sub = CSR(a.nrows, min(width, a.ncols - k * width), brp.to(torch.int32), c.to(torch.int32), v)
+        blocks.append(to_csr_aligned(sub).to(a.rp.device))
+        col0.append(k * width)
+    return CSRColBlocked(a.nrows, a.ncols, tuple(col0), tuple(blocks))
+
+
+@dataclass
 class ELL:
     nrows: int
     ncols: int
@@ -277,6 +322,10 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
                       x.data_ptr(), y.data_ptr(), float(beta))
         return y
     s = _ext.stream_ptr(x.device)
+    if isinstance(a, CSRColBlocked):
+        for k, (c0, b) in enumerate(zip(a.col0, a.blocks)):
+            spmv(b, x[c0:c0 + b.ncols], y, kernel=kernel, beta=beta if k == 0 else 1.0)
+        return y
     if isinstance(a, CSRAligned):
         g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
         _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
@@ -356,6 +405,7 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
     if fmt == "auto":
         fmt = choose_format(a)
     conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_aligned": to_csr_aligned,
+            "csr_cb": to_csr_colblocked,
             "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}
     if fmt not in conv:
         raise ValueError(f"unknown SpMV format {fmt!r}")
@@ -366,4 +416,4 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
 def bytes_per_nnz(fmt: str) -> float:
     """Bell & Garland's fp32 byte model per nonzero (their Table: DIA 4,
     ELL 6... here value + index bytes): for GFLOP/s -> GB/s conversions."""
-    return {"dia": 4, "ell": 8, "csr": 8, "coo": 12, "hyb": 8}[fmt]
+    return {"dia": 4, "ell": 8, "csr": 8, "coo": 12, "hyb": 8, "csr_cb": 8}[fmt]

@@ -40,6 +40,10 @@ def tensors_of(m):
                 out.append(v)
             elif is_dataclass(v):
                 out.extend(tensors_of(v))
+            elif isinstance(v, tuple):  # column blocks
+                for e in v:
+                    if is_dataclass(e):
+                        out.extend(tensors_of(e))
     return out
 
 
@@ -56,6 +60,8 @@ def clone(m):
             kw[f.name] = v.clone()
         elif is_dataclass(v):
             kw[f.name] = clone(v)
+        elif isinstance(v, tuple) and v and is_dataclass(v[0]):
+            kw[f.name] = tuple(clone(e) for e in v)
     return replace(m, **kw)
 
 

@@ -3,8 +3,8 @@ import numpy as np
 import pytest
 import torch
 
-from cme213x.ops.spmv import (CSR, hyb_k, laplacian, random_csr, spmv, to_coo, to_csr_aligned, to_dia, to_ell,
-                               to_hyb)
+from cme213x.ops.spmv import (CSR, hyb_k, laplacian, random_csr, spmv, to_coo, to_csr_aligned, to_csr_colblocked,
+                               to_dia, to_ell, to_hyb)
 
 
 def _ref(a: CSR, x):
@@ -42,7 +42,7 @@ def test_csr_cpu_and_conversions():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
-@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_aligned", "ell", "dia", "coo", "hyb"])
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_aligned", "ell", "dia", "coo", "hyb", "csr_cb"])
 def test_spmv_gpu(gpu, mat, fmt):
     if mat == "5pt":
         a = laplacian("5pt", 100)
@@ -56,6 +56,15 @@ def test_spmv_gpu(gpu, mat, fmt):
         pytest.skip("DIA only for structured matrices")
     x = torch.randn(a.ncols)
     ref = _ref(a, x)
+    if fmt == "csr_cb":  # column blocks of 4 KB of x: several blocks even at these sizes
+        dev = to_csr_colblocked(a, block_bytes=4096).to(gpu)
+        assert len(dev.blocks) > 1 and dev.col0[0] == 0
+        y = spmv(dev, x.to(gpu)).cpu().numpy()
+        np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+        y0 = torch.randn(a.nrows, device=gpu)
+        y1 = spmv(dev, x.to(gpu), y0.clone(), beta=0.5).cpu().numpy()
+        np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
+        return
     dev = {"csr_scalar": a, "csr_vector": a, "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
            "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
            "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
