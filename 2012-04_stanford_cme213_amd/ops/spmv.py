@@ -106,9 +106,11 @@ class CSRColBlocked:
         return CSRColBlocked(self.nrows, self.ncols, self.col0, tuple(b.to(device) for b in self.blocks))
 
 
-def to_csr_colblocked(a: CSR, block_bytes: int = 2 << 20) -> CSRColBlocked:
+def to_csr_colblocked(a: CSR, block_bytes: int = 2 << 20, aligned: bool = True) -> CSRColBlocked:
     """Split ``a`` into ceil(4 * ncols / block_bytes) column blocks of equal
-    width (aligned CSR each; column indices made block-relative)."""
+    width (column indices made block-relative), each an aligned CSR (rows
+    padded to multiples of 4 entries) or, ``aligned=False``, a plain CSR
+    (no padding; CSR-vector kernel)."""
     nb = max(1, -(-4 * a.ncols // block_bytes))
     width = -(-a.ncols // nb)
     rp = a.rp.cpu().long()
@@ -123,7 +125,7 @@ def to_csr_colblocked(a: CSR, block_bytes: int = 2 << 20) -> CSRColBlocked:
         brp = torch.zeros(a.nrows + 1, dtype=torch.long)
         brp[1:] = torch.cumsum(torch.bincount(r, minlength=a.nrows), 0)
         sub = CSR(a.nrows, min(width, a.ncols - k * width), brp.to(torch.int32), c.to(torch.int32), v)
-        blocks.append(to_csr_aligned(sub).to(a.rp.device))
+        blocks.append((to_csr_aligned(sub) if aligned else sub).to(a.rp.device))
         col0.append(k * width)
     return CSRColBlocked(a.nrows, a.ncols, tuple(col0), tuple(blocks))
 
@@ -404,6 +406,10 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
     returns (format name, matrix) ready for :func:`spmv`."""
     if fmt == "auto":
         fmt = choose_format(a)
+    if fmt.startswith("csr_cb_"):  # csr_cb_<KiB of x per block>[_u]: sweep arms of the column-blocked CSR
+        parts = fmt.split("_")[2:]
+        m = to_csr_colblocked(a, int(parts[0]) << 10, aligned=not (len(parts) > 1 and parts[1] == "u"))
+        return fmt, (m.to(device) if device is not None else m)
     conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_aligned": to_csr_aligned,
             "csr_cb": to_csr_colblocked,
             "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}
