@@ -390,7 +390,9 @@ def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
       * ELL  -- regular rows (max row length close to the mean);
       * HYB  -- ELL for the typical rows + COO for a heavy tail (power-law
                 rows would serialise CSR lanes on the longest row);
-      * CSR-vector (16-B aligned rows) -- everything else."""
+      * CSR-vector (16-B aligned rows) -- everything else, in column blocks of
+        2 MB of x when x is larger (one XCD's L2 keeps the block's x slice:
+        random 1M x 1M, 16/row: 0.0957 vs 0.1038 ms cold, profiles/spmv_cb_r3.jsonl)."""
     st = stats or matrix_stats(a)
     if st.ndiag <= 64 and st.dia_fill >= 0.6:
         return "dia"
@@ -398,7 +400,7 @@ def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
         return "ell"
     if st.max_row > 8 * max(1.0, st.mean_row) or st.cv_row > 1.0:
         return "hyb"
-    return "csr_aligned"
+    return "csr_cb" if 4 * a.ncols > (2 << 20) else "csr_aligned"
 
 
 def prepare(a: CSR, fmt: str = "auto", device=None):

@@ -118,7 +118,7 @@ def main():
         A = gens[name]()
         st = matrix_stats(A)
         auto = choose_format(A, st)
-        fmts = args.fmts or ["csr_scalar", "csr_vector", "csr_aligned", "coo", "hyb", "ell", "dia"]
+        fmts = args.fmts or ["csr_scalar", "csr_vector", "csr_aligned", "csr_cb", "coo", "hyb", "ell", "dia"]
         res = {}
         for f in fmts:
             if f == "ell" and (st.max_row > 64 or st.ell_fill < 0.3):
@@ -172,7 +172,7 @@ def main():
                  ms_warm=round(ms_warm, 5), GFLOPs_cold=round(2 * A.nnz / ms_cold / 1e6, 1),
                  GFLOPs_warm=round(2 * A.nnz / ms_warm / 1e6, 1), min_bytes=mb1,
                  GBps_cold=round(mb1 / ms_cold / 1e6, 1), pct_copy_cold=round(100 * mb1 / ms_cold / 1e6 / copy_GBps, 1),
-                 auto=(f == auto or (auto == "csr_aligned" and f == "csr_aligned")))
+                 auto=(f == auto))
             del sets
             torch.cuda.empty_cache()
         best = min(res, key=res.get)
