@@ -66,6 +66,11 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, 4, RB, 1, true, 1, 8, 4>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                                chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 91:  // wide lanes, reassociated ("fast") arithmetic: 17 instead of 20 flop-instructions per point
+            if constexpr (RB == 2 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, 2, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
         case 84:
             if constexpr (RB == 2 && NS == 4) {

@@ -268,7 +268,8 @@ def test_fast_oracle_close_to_exact():
 @pytest.mark.gpu
 def test_gpu_pipe_fast_arms_bitwise(gpu):
     """The reassociated-arithmetic tuning arms (pd 12: default registers, 13:
-    capped at 4 waves/SIMD) equal ns steps of the CPU fast oracle bit for bit."""
+    capped at 4 waves/SIMD, 91: wide lanes) equal ns steps of the CPU fast
+    oracle bit for bit."""
     from cme213x import _ext
     p = SimParams(nx=1500, ny=700, order=8)
     c = _rand_grid(p, torch.float32, seed=9)
@@ -277,10 +278,10 @@ def test_gpu_pipe_fast_arms_bitwise(gpu):
     s = _ext.stream_ptr(g.buf[0].device)
     for ns in (3, 4):
         oracle = _fast_steps(c, region, ns)
-        for pd in (12, 13):
+        for pd, rb in ((12, 4), (13, 4), (91, 2)):  # 91: wide lanes
             out = g.buf[0].clone()
             _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, *region,
-                          g.xcfl, g.ycfl, 0, 4, ns, pd, 0, s)
+                          g.xcfl, g.ycfl, 0, rb, ns, pd, 0, s)
             torch.cuda.synchronize()
             assert torch.equal(out.cpu(), oracle), (ns, pd)
 
