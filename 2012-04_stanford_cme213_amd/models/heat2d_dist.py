@@ -165,6 +165,43 @@ def auto_kernel(dtype, points: int, tblock: int) -> str:
     return "streamn"
 
 
+class CheckpointWriter:
+    """Background writer of :meth:`DistHeat.checkpoint_async` (one thread:
+    wait for the device-to-host copy, then one safetensors file per
+    subdomain)."""
+
+    def __init__(self, directory: str, items: list, event=None):
+        import os
+        import threading
+
+        self.paths = [os.path.join(directory, f"heat_rank{r}.safetensors") for r, *_ in items]
+        self._items, self._event, self._error = items, event, None
+        self._thread = threading.Thread(target=self._write, daemon=True)
+        self._thread.start()
+
+    def _write(self) -> None:
+        from ..utils.gridio import save_checkpoint
+
+        try:
+            if self._event is not None:
+                self._event.synchronize()
+            for path, (r, t, meta, _) in zip(self.paths, self._items):
+                save_checkpoint(path, {"interior": t.numpy()}, meta)
+        except Exception as e:  # noqa: BLE001 - re-raised by wait()
+            self._error = e
+        finally:
+            self._items = None  # release the pinned buffers and snapshots
+
+    def done(self) -> bool:
+        return not self._thread.is_alive()
+
+    def wait(self) -> list[str]:
+        self._thread.join()
+        if self._error is not None:
+            raise self._error
+        return self.paths
+
+
 class DistHeat:
     """Distributed heat solver. ``local_ranks`` lists the subdomains owned by
     this process (default: ``[comm.rank]``); ``world`` is the total number of
@@ -611,6 +648,40 @@ class DistHeat:
             save_checkpoint(path, {"interior": own}, self._meta(r))
             paths.append(path)
         return paths
+
+    def checkpoint_async(self, directory: str) -> "CheckpointWriter":
+        """:meth:`checkpoint` off the critical path. The owned interiors are
+        snapshotted on the device (one device copy each, waited for before
+        returning, so the time loop may overwrite the grids at once); the
+        snapshots go to pinned host memory on a side stream and a background
+        thread writes the same files as :meth:`checkpoint` once that copy has
+        landed. ``.wait()`` returns the paths (and re-raises a write error)."""
+        import os
+
+        self.finish()
+        os.makedirs(directory, exist_ok=True)
+        snaps = []
+        for r, s in self.subs.items():
+            g = s.grid
+            H = g.H
+            snaps.append((r, g.buf[g.cur, H:H + g.ny, H:H + g.nx].clone(), self._meta(r)))
+        event = None
+        if self.device.type == "cuda":
+            cur = torch.cuda.current_stream(self.device)
+            cur.synchronize()  # snapshots complete: the grids are free again
+            side = torch.cuda.Stream(self.device)
+            host = []
+            with torch.cuda.stream(side):
+                for r, snap, meta in snaps:
+                    h = torch.empty(snap.shape, dtype=snap.dtype, pin_memory=True)
+                    h.copy_(snap, non_blocking=True)
+                    host.append((r, h, meta, snap))  # snap kept alive until the copy is done
+            event = torch.cuda.Event()
+            event.record(side)
+            snaps = host
+        else:
+            snaps = [(r, t, meta, None) for r, t, meta in snaps]
+        return CheckpointWriter(directory, snaps, event)
 
     def restore(self, directory: str) -> None:
         """Load :meth:`checkpoint` files written by a run with the same global

@@ -276,7 +276,7 @@ def test_dist_spmv_scan_gloo(world):
     assert e["relL2"] < 1e-5, e
 
 
-def _ckpt_rank(rank, world, directory, tblock):
+def _ckpt_rank(rank, world, directory, tblock, use_async=False):
     import cme213x
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.parallel.comm import TorchComm
@@ -292,8 +292,13 @@ def _ckpt_rank(rank, world, directory, tblock):
         g.buf[:, g.H:g.H + b.ny, g.H:g.H + b.nx] = torch.from_numpy(np.sin(0.3 * xx) * np.cos(0.2 * yy) + 5.0)
     full.exchange(full._cur()).wait()
     full.run(5)
-    full.checkpoint(directory)
-    full.run(6)
+    if use_async:  # the run continues while the files are written
+        w = full.checkpoint_async(directory)
+        full.run(6)
+        assert len(w.wait()) == len(full.subs)
+    else:
+        full.checkpoint(directory)
+        full.run(6)
     # a fresh solver resumes from the checkpoint and must land on the same state
     resumed = DistHeat(p, c, torch.float64, "cpu", variant="naive", tblock=tblock)
     resumed.restore(directory)
@@ -305,6 +310,6 @@ def _ckpt_rank(rank, world, directory, tblock):
     return bool(np.array_equal(a.state()[B:-B, B:-B], b.state()[B:-B, B:-B]))
 
 
-@pytest.mark.parametrize("tblock", [1, 2, 4])
-def test_dist_heat_checkpoint_restart_gloo(tmp_path, tblock):
-    assert all(run_ranks(_ckpt_rank, 4, (str(tmp_path), tblock)))
+@pytest.mark.parametrize("tblock,use_async", [(1, False), (2, False), (4, False), (2, True)])
+def test_dist_heat_checkpoint_restart_gloo(tmp_path, tblock, use_async):
+    assert all(run_ranks(_ckpt_rank, 4, (str(tmp_path), tblock, use_async)))

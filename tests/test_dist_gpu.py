@@ -157,8 +157,9 @@ def test_pipe_kernel_subdomains_gpu(gpu, method, world, sync, tblock, fma, nativ
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tblock,fma", [(1, False), (2, True), (4, True)])
-def test_native_loop_checkpoint_restart_gpu(gpu, tmp_path, tblock, fma):
+@pytest.mark.parametrize("tblock,fma,use_async", [(1, False, False), (2, True, False), (4, True, False),
+                                                  (4, True, True)])
+def test_native_loop_checkpoint_restart_gpu(gpu, tmp_path, tblock, fma, use_async):
     """Native loop on GPU subdomains: run 3, checkpoint, run 4 more; a fresh
     solver restored from the checkpoint and run 4 must land on the same
     state bit for bit (halos rebuilt by restore's exchange)."""
@@ -170,8 +171,13 @@ def test_native_loop_checkpoint_restart_gpu(gpu, tmp_path, tblock, fma):
     mk = lambda: DistHeat(p, None, torch.float32, gpu, local_ranks=list(range(4)), world=4, tblock=tblock, fma=fma)
     full = mk()
     full.run_native(3)
-    full.checkpoint(str(tmp_path))
-    full.run_native(4)
+    if use_async:  # snapshot, then the run continues while the files are written
+        w = full.checkpoint_async(str(tmp_path))
+        full.run_native(4)
+        w.wait()
+    else:
+        full.checkpoint(str(tmp_path))
+        full.run_native(4)
     resumed = mk()
     resumed.restore(str(tmp_path))
     assert resumed.iteration == 3
