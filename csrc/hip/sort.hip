@@ -121,14 +121,23 @@ __global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__
 }
 
 // Stable rank of each lane's digit among the lanes of its wave (ballot match).
+// Per bit: the lane's bit as an all-ones / zero mask (one signed bit-field
+// extract), its ballot, and peers &= ~(ballot ^ mask) (keep the lanes whose
+// bit agrees) -- an and-xnor of three operands, one gfx950 v_bitop3_b32 per
+// 32-bit half, instead of a select between the ballot and its complement.
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
-    uint64_t peers = __ballot(valid);
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
     for (int b = 0; b < kRadixBits; ++b) {
-        const uint64_t m = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? m : ~m;
+        uint32_t s;  // 0 or ~0: one signed bit-field extract (the compiler otherwise emits a shift pair)
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(s) : "v"(d), "i"(b));
+        const uint64_t m = __ballot(s != 0u);
+        // truth table of peers & ~(m ^ s) over (src0, src1, src2) = (0xf0, 0xcc, 0xaa)
+        lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)m, s, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(m >> 32), s, 0x90);
     }
-    return peers;
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // ATOMIC_RANK: in-wave ranks through returning LDS atomics issued back to
