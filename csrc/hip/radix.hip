@@ -116,14 +116,21 @@ __global__ __launch_bounds__(kHistThreads) void radix_hist_kernel(const uint32_t
 }
 
 // Stable rank of each lane's digit among the lanes of its wave (ballot match).
+// (per bit: the bit as an all-ones / zero mask, its ballot, and one gfx950
+// v_bitop3_b32 per 32-bit half for peers &= ~(ballot ^ mask); sort.hip
+// match_digit, profiles/sort_r3.md)
 __device__ __forceinline__ uint64_t os_match(uint32_t d, bool valid) {
-    uint64_t peers = __ballot(valid);
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-        const uint64_t m = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? m : ~m;
+        uint32_t s;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(s) : "v"(d), "i"(b));
+        const uint64_t m = __ballot(s != 0u);
+        lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)m, s, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(m >> 32), s, 0x90);
     }
-    return peers;
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // ---------------------------------------------------------------- K1..KP
