@@ -195,10 +195,9 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
         if (!PREFETCH) load_tile(t0);
         const int nk = items_of(t0);
         __syncthreads();
-        if (mode_in) {
+        if (mode_in) {  // every item: an invalid item's code is never ranked (outside the valid ballot)
 #pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if (k < nk) key[k] = rx_key_in(key[k], mode_in);
+            for (int k = 0; k < kItems; ++k) key[k] = rx_key_in(key[k], mode_in);
         }
         if constexpr (!ATOMIC_RANK) {
 #pragma unroll
