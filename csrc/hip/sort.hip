@@ -159,6 +159,7 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
     __shared__ uint32_t s_whist[kWavesD][kBins];  // per-wave running counts, then exclusive prefixes
     __shared__ uint32_t s_tile_off[kBins];            // exclusive prefix of tile digit counts
     __shared__ uint32_t s_base[kBins];                // global position of the next key of each digit
+    __shared__ uint32_t s_gdiff[kBins];               // s_base - s_tile_off: tile index -> global position
     const int lane = lane_id();
     const int wid = threadIdx.x / kWave;
     const long long b0 = (long long)blockIdx.x * chunk;
@@ -257,7 +258,10 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
             const uint32_t c = tid < kBins ? s_tile_off[tid] : 0u;
             const uint32_t ex = block_exclusive_scan<kWavesD>(c, s_tmp, tot, OpAdd());
             __syncthreads();
-            if (tid < kBins) s_tile_off[tid] = ex;
+            if (tid < kBins) {
+                s_tile_off[tid] = ex;
+                s_gdiff[tid] = s_base[tid] - ex;
+            }
         }
         __syncthreads();
         // reorder the tile by digit in LDS
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
         for (int i = threadIdx.x; i < tile_n; i += DS_THREADS) {
             const uint32_t k = s_keys[i];
             const uint32_t d = digit_of(k, shift);
-            const uint32_t g = s_base[d] + (uint32_t)i - s_tile_off[d];
+            const uint32_t g = s_gdiff[d] + (uint32_t)i;
             keys_out[g] = rx_key_out(k, mode_out);
             if constexpr (HAS_VALUES) vals_out[g] = s_vals[i];
         }
