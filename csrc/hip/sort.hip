@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
     // UNR 16-B loads in flight per lane before their LDS atomics (one load at
     // a time left the kernel waiting on HBM latency: wait-any 0.85 of its
     // cycles, profiles/sort_r3.md)
-    constexpr int UNR = 8;
+    constexpr int UNR = 4;
     constexpr long long STEP = (long long)kSortThreads * 4;
     long long i = b0 + threadIdx.x * 4;
     if (vec) {
