@@ -306,3 +306,22 @@ def test_hw2_driver_cpu(tmp_path):
     res = run_hw2(str(f), device="cpu", outdir=str(tmp_path))
     assert res["cpu_ms"] >= 0
     assert (tmp_path / "grid_init.txt").exists()
+
+
+def test_checkpoint_writer_reports_errors(tmp_path):
+    """A write error of the background checkpoint writer is raised by wait(),
+    and a good writer returns its paths with the files complete."""
+    import numpy as np
+
+    from cme213x.models.heat2d_dist import CheckpointWriter
+    from cme213x.utils.gridio import load_checkpoint
+
+    t = torch.arange(12, dtype=torch.float32).reshape(3, 4)
+    ok = CheckpointWriter(str(tmp_path), [(0, t, {"iteration": 3}, None)])
+    paths = ok.wait()
+    assert ok.done() and len(paths) == 1
+    got, meta = load_checkpoint(paths[0])
+    assert np.array_equal(got["interior"], t.numpy()) and meta["iteration"] == "3"
+    bad = CheckpointWriter(str(tmp_path / "missing" / "dir"), [(0, t, {"iteration": 3}, None)])
+    with pytest.raises(Exception):
+        bad.wait()

@@ -75,3 +75,27 @@ def test_spmv_gpu(gpu, mat, fmt):
     y0 = torch.randn(a.nrows, device=gpu)
     y1 = spmv(dev, x.to(gpu), y0.clone(), kernel=kernel, beta=0.5).cpu().numpy()
     np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
+
+
+def test_colblocked_format_choice_and_blocks():
+    """Column-blocked CSR: block count from the x footprint (2 MB per block),
+    block-relative columns, and `auto` choosing it only when x exceeds 2 MB
+    (random rows; structured matrices keep DIA / ELL)."""
+    from cme213x.ops.spmv import choose_format, to_csr_colblocked
+
+    small = random_csr(300, 4096, 12, seed=4)
+    assert choose_format(small) == "csr_aligned"
+    big = random_csr(2000, 1 << 20, 12, seed=5)  # x = 4 MB: two 2 MB blocks
+    assert choose_format(big) == "csr_cb"
+    cb = to_csr_colblocked(big)
+    assert cb.col0 == (0, 1 << 19) and all(b.ncols == 1 << 19 for b in cb.blocks)
+    for b in cb.blocks:
+        assert int(b.col.max()) < b.ncols and int(b.col.min()) >= 0
+    # the blocks partition the entries: every (row, global column, value) once (padding has value 0)
+    got = sorted((r, c0 + int(c), float(v)) for c0, b in zip(cb.col0, cb.blocks)
+                 for r, (s, e) in enumerate(zip(b.rp[:-1].tolist(), b.rp[1:].tolist()))
+                 for c, v in zip(b.col[s:e].tolist(), b.val[s:e].tolist()) if v != 0.0)
+    rows = np.repeat(np.arange(big.nrows), np.diff(big.rp.numpy()))
+    want = sorted(zip(rows.tolist(), big.col.tolist(), big.val.tolist()))
+    assert got == want
+    assert choose_format(laplacian("5pt", 1100)) == "dia"
