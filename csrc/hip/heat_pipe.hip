@@ -77,6 +77,21 @@ namespace {
 template <int ORDER, bool FMA>
 int pipe_ns_f64(const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, double xcfl,
                 double ycfl, int chunk, hipStream_t s, PipeGate gate) {
+    // FMA: the chains of a lane's 4 points issued term by term (bitwise the
+    // same; CME_PIPE_TM64=0 keeps them chain by chain for A/B runs)
+    static const bool tm = [] {
+        const char* e = getenv("CME_PIPE_TM64");
+        return !(e && atoi(e) == 0);
+    }();
+    if constexpr (FMA) {
+        if (tm) {
+            switch (ns) {
+                case 3: return launch_pipe_multi<double, ORDER, 3, 4, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+                case 4: return launch_pipe_multi<double, ORDER, 4, 4, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
+                default: return (int)hipErrorInvalidValue;
+            }
+        }
+    }
     switch (ns) {
         case 3: return launch_pipe_multi<double, ORDER, 3, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         case 4: return launch_pipe_multi<double, ORDER, 4, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
