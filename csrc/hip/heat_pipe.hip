@@ -77,11 +77,12 @@ namespace {
 template <int ORDER, bool FMA>
 int pipe_ns_f64(const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, double xcfl,
                 double ycfl, int chunk, hipStream_t s, PipeGate gate) {
-    // FMA: the chains of a lane's 4 points issued term by term (bitwise the
-    // same; CME_PIPE_TM64=0 keeps them chain by chain for A/B runs)
+    // CME_PIPE_TM64=1: issue the FMA chains of a lane's 4 points term by term
+    // (bitwise the same; the fp32 wide pass's order). Off by default until
+    // measured on the fp64 shapes (the round-3 session ran out of GPU boxes).
     static const bool tm = [] {
         const char* e = getenv("CME_PIPE_TM64");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) == 1;
     }();
     if constexpr (FMA) {
         if (tm) {
