@@ -25,9 +25,8 @@ def heat2d_main(argv=None) -> int:
 
 
 def heat2d_mpi_main(argv=None) -> int:
-    from ..models.heat2d_dist import DistHeat, run_hw5
+    from ..models.heat2d_dist import run_hw5
     from ..parallel.comm import init_from_env
-    from ..utils.params import SimParams
 
     ap = argparse.ArgumentParser(prog="heat2d_mpi")
     ap.add_argument("params")
@@ -37,26 +36,26 @@ def heat2d_mpi_main(argv=None) -> int:
     ap.add_argument("--tblock", default="auto", help="timesteps per halo exchange / HBM pass (1-4, or auto)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "pipe", "streamn"], help="3-4 step pass kernel")
     ap.add_argument("--fma", action="store_true", help="FMA-contracted stencil (the reference CPU's is not)")
+    ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
+                    help="GPU time loop: the native C++ loop after a bitwise self-test (auto), required (on), "
+                         "or the Python loop (off)")
+    ap.add_argument("--transport", default=None, choices=["rccl", "ipc"],
+                    help="native halo transport under torchrun (default: rccl on nccl, ipc with --share-gpu)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="under torchrun: every rank on cuda:0, gloo control plane, IPC halo transport "
+                         "(rehearses the multi-process run on one GPU)")
+    ap.add_argument("--periodic", default="", choices=["", "x", "y", "xy"],
+                    help="wrap the decomposition along x / y (not in the reference; with one rank every halo "
+                         "is a self-send)")
     a = ap.parse_args(argv)
     tblock = a.tblock if a.tblock == "auto" else int(a.tblock)
     dtype = torch.float32 if a.float else torch.float64
+    periodic = ("x" in a.periodic, "y" in a.periodic)
     if a.ranks:
-        import time
-
-        p = SimParams.from_file(a.params, flavor="hw5")
-        print(p.banner())
-        dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-        sim = DistHeat(p, None, dtype, dev, local_ranks=list(range(a.ranks)), world=a.ranks, tblock=tblock,
-                       fma=a.fma, kernel=a.kernel)
-        sim.save_text("init")
-        t0 = time.perf_counter()
-        sim.run(p.iters)
-        if torch.device(dev).type == "cuda":
-            torch.cuda.synchronize()
-        print(f"{p.iters} iterations on a {p.nx} by {p.ny} grid took: {time.perf_counter() - t0} seconds.")
-        sim.save_text("final")
+        run_hw5(a.params, None, dtype, a.device, tblock=tblock, fma=a.fma, kernel=a.kernel, native=a.native,
+                local_ranks=list(range(a.ranks)), world=a.ranks, periodic=periodic)
         return 0
-    comm = init_from_env()
-    dev = a.device or ("cuda" if torch.cuda.is_available() else "cpu")
-    run_hw5(a.params, comm, dtype, dev, tblock=tblock, fma=a.fma, kernel=a.kernel)
+    comm = init_from_env(backend="gloo" if a.share_gpu else None, share_gpu=a.share_gpu)
+    run_hw5(a.params, comm, dtype, a.device, tblock=tblock, fma=a.fma, kernel=a.kernel, native=a.native,
+            periodic=periodic, transport=a.transport or ("ipc" if a.share_gpu else None))
     return 0

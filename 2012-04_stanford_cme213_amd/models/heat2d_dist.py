@@ -165,6 +165,21 @@ def auto_kernel(dtype, points: int, tblock: int) -> str:
     return "streamn"
 
 
+def _save_atomic(path: str, tensors: dict, meta: dict) -> None:
+    """Write a checkpoint file under a temporary name, then rename it over
+    ``path``: a crash mid-write leaves the previous checkpoint intact."""
+    import os
+
+    from ..utils.gridio import save_checkpoint
+
+    tmp = f"{path}.tmp{os.getpid()}"
+    save_checkpoint(tmp, tensors, meta)
+    os.replace(tmp, path)
+
+
+_ACTIVE_WRITERS: dict = {}  # realpath(directory) -> CheckpointWriter still writing
+
+
 class CheckpointWriter:
     """Background writer of :meth:`DistHeat.checkpoint_async` (one thread:
     wait for the device-to-host copy, then one safetensors file per
@@ -176,17 +191,22 @@ class CheckpointWriter:
 
         self.paths = [os.path.join(directory, f"heat_rank{r}.safetensors") for r, *_ in items]
         self._items, self._event, self._error = items, event, None
+        # one writer per directory at a time: a new checkpoint into the same
+        # files waits for the previous one (no interleaved per-rank files)
+        key = os.path.realpath(directory)
+        prev = _ACTIVE_WRITERS.get(key)
+        if prev is not None and prev is not self:
+            prev._thread.join()
+        _ACTIVE_WRITERS[key] = self
         self._thread = threading.Thread(target=self._write, daemon=True)
         self._thread.start()
 
     def _write(self) -> None:
-        from ..utils.gridio import save_checkpoint
-
         try:
             if self._event is not None:
                 self._event.synchronize()
             for path, (r, t, meta, _) in zip(self.paths, self._items):
-                save_checkpoint(path, {"interior": t.numpy()}, meta)
+                _save_atomic(path, {"interior": t.numpy()}, meta)
         except Exception as e:  # noqa: BLE001 - re-raised by wait()
             self._error = e
         finally:
@@ -209,16 +229,28 @@ class DistHeat:
 
     def __init__(self, params: SimParams, comm: Comm | None = None, dtype=torch.float32, device="cpu",
                  local_ranks: list[int] | None = None, world: int | None = None, variant: str = "stream",
-                 tblock: int | str = 1, fma: bool = False, kernel: str = "streamn"):
+                 tblock: int | str = 1, fma: bool = False, kernel: str = "streamn",
+                 periodic: tuple[bool, bool] = (False, False), native: str = "off"):
         self.p = params
         self.comm = comm or LoopbackComm()
         self.world = world or self.comm.size
         self.local_ranks = local_ranks if local_ranks is not None else [self.comm.rank]
+        self.periodic = (bool(periodic[0]), bool(periodic[1]))
         if self.comm.size > 1 and (len(self.local_ranks) != 1 or self.world != self.comm.size):
             raise ValueError("multi-process runs own exactly one subdomain per rank")
-        if tblock == "auto" or kernel == "auto":  # by the (largest) subdomain's size
-            pts = max(b.nx * b.ny for b in (decompose(params.nx, params.ny, self.world, params.grid_method, r)
-                                            for r in self.local_ranks))
+        if native not in ("off", "auto", "on"):
+            raise ValueError("native must be 'off', 'auto' or 'on'")
+        # run(): the native C++ time loop after a one-time bitwise self-test
+        # ("auto": fall back to the Python loop if it fails; "on": raise)
+        self.native_mode = native
+        self.native_info: dict | None = None
+        if tblock == "auto" or kernel == "auto":
+            # by the LARGEST subdomain of the whole decomposition -- the same
+            # answer on every rank (an uneven split must not give neighbours
+            # different halo depths / exchange cadences)
+            pts = max(b.nx * b.ny for b in (decompose(params.nx, params.ny, self.world, params.grid_method, r,
+                                                      self.periodic)
+                                            for r in range(self.world)))
             if tblock == "auto":
                 tblock = auto_tblock(dtype, pts, fma, torch.device(device).type)
             if kernel == "auto":
@@ -238,7 +270,7 @@ class DistHeat:
         self.device = torch.device(device)
         self.subs: dict[int, _Sub] = {}
         for r in self.local_ranks:
-            blk = decompose(params.nx, params.ny, self.world, params.grid_method, r)
+            blk = decompose(params.nx, params.ny, self.world, params.grid_method, r, self.periodic)
             g = HeatGrid(params, dtype, device, nx=blk.nx, ny=blk.ny, bc_sides=blk.bc_sides,
                          halo=tblock * params.border)
             self.subs[r] = _Sub(blk, g, corners=tblock > 1)
@@ -256,11 +288,22 @@ class DistHeat:
 
     # -- halo exchange ---------------------------------------------------
     def exchange(self, k: int) -> Pending:
-        """Fill the ghost cells of state ``k`` from the neighbours' borders."""
-        ops: list[P2P] = []
+        """Fill the ghost cells of state ``k`` from the neighbours' borders.
+
+        Remote pieces are posted in the canonical halo order of the native
+        plan (:meth:`_sub_plan`): sends as rows (top, bottom) then blocks
+        (left, corners, right); receives in the REVERSED order of each group.
+        The block order is its own mirror (piece i and piece n-1-i face
+        opposite ways), so the k-th send to a peer always meets the k-th
+        receive from us on the peer -- also when one peer sits on several
+        sides (periodic grids with one or two blocks along an axis, where
+        per-peer FIFO matching of same-side pieces would swap the halos)."""
+        sends: list[P2P] = []
+        recvs: list[P2P] = []
         post_unpack = []
         for r, s in self.subs.items():
             blk = s.blk
+            row_recv, blk_recv = [], []
             for side in ("top", "bottom"):
                 peer = getattr(blk, side)
                 if peer < 0:
@@ -268,30 +311,30 @@ class DistHeat:
                 if peer in self.subs:
                     self.subs[peer].row_recv(k, _OPP[side]).copy_(s.row_send(k, side))
                 else:
-                    ops.append(P2P("send", s.row_send(k, side), peer))
-                    ops.append(P2P("recv", s.row_recv(k, side), peer))
-            for side in ("left", "right"):
-                peer = getattr(blk, side)
+                    sends.append(P2P("send", s.row_send(k, side), peer))
+                    row_recv.append(P2P("recv", s.row_recv(k, side), peer))
+            pieces = [("left", blk.left)] + [((dx, dy), p) for (dx, dy), p in s.diag.items()] + [("right", blk.right)]
+            for key, peer in pieces:
                 if peer < 0:
                     continue
-                if peer in self.subs:
-                    self.subs[peer].col_recv_view(k, _OPP[side]).copy_(s.col_send_view(k, side))
+                if isinstance(key, str):
+                    send_v, recv_v = s.col_send_view(k, key), s.col_recv_view(k, key)
+                    if peer in self.subs:
+                        self.subs[peer].col_recv_view(k, _OPP[key]).copy_(send_v)
+                        continue
                 else:
-                    sbuf, rbuf = s.stage[side]
-                    sbuf.copy_(s.col_send_view(k, side))
-                    ops.append(P2P("send", sbuf, peer))
-                    ops.append(P2P("recv", rbuf, peer))
-                    post_unpack.append((s.col_recv_view(k, side), rbuf))
-            for (dx, dy), peer in s.diag.items():
-                if peer in self.subs:
-                    self.subs[peer].corner_view(k, -dx, -dy, False).copy_(s.corner_view(k, dx, dy, True))
-                else:
-                    sbuf, rbuf = s.stage[(dx, dy)]
-                    sbuf.copy_(s.corner_view(k, dx, dy, True))
-                    ops.append(P2P("send", sbuf, peer))
-                    ops.append(P2P("recv", rbuf, peer))
-                    post_unpack.append((s.corner_view(k, dx, dy, False), rbuf))
-        pend = self.comm.exchange(ops)
+                    dx, dy = key
+                    send_v, recv_v = s.corner_view(k, dx, dy, True), s.corner_view(k, dx, dy, False)
+                    if peer in self.subs:
+                        self.subs[peer].corner_view(k, -dx, -dy, False).copy_(send_v)
+                        continue
+                sbuf, rbuf = s.stage[key]
+                sbuf.copy_(send_v)
+                sends.append(P2P("send", sbuf, peer))
+                blk_recv.append(P2P("recv", rbuf, peer))
+                post_unpack.append((recv_v, rbuf))
+            recvs += row_recv[::-1] + blk_recv[::-1]
+        pend = self.comm.exchange(sends + recvs)
         if not post_unpack:
             return pend
 
@@ -391,17 +434,24 @@ class DistHeat:
                 send = (ny if side == "top" else H) * pitch
                 recv = (ny + H if side == "top" else 0) * pitch
                 rows.append((peer, send, recv, H * pitch))
-        # staged blocks: {peer, send_x, send_y, recv_x, recv_y, rows, width}
-        for side in ("left", "right"):
-            peer = getattr(b, side)
-            if peer >= 0:
-                sx = nx if side == "right" else H
-                rx = nx + H if side == "right" else 0
-                cols.append((peer, sx, H, rx, H, ny, H))
+        # staged blocks: {peer, send_x, send_y, recv_x, recv_y, rows, width},
+        # in the mirrored canonical order of exchange(): left, the corners
+        # (-1,-1) (-1,1) (1,-1) (1,1), right -- block i and block n-1-i face
+        # opposite ways, which is what lets the native transports post the
+        # receives in reverse order and match repeated peers correctly
+        def col(side):
+            sx = nx if side == "right" else H
+            rx = nx + H if side == "right" else 0
+            return (getattr(b, side), sx, H, rx, H, ny, H)
+
+        if b.left >= 0:
+            cols.append(col("left"))
         for (dx, dy), peer in s.diag.items():
             sx, sy = s.corner_origin(dx, dy, True)
             rx, ry = s.corner_origin(dx, dy, False)
             cols.append((peer, sx, sy, rx, ry, H, H))
+        if b.right >= 0:
+            cols.append(col("right"))
         stage_elems = 2 * sum(c[5] * c[6] for c in cols)
         return {
             "interior": torch.tensor(np.array(interior, dtype=np.int32).reshape(-1, 4)),
@@ -469,19 +519,23 @@ class DistHeat:
             d.stage = ipc.open(*pi["stage"])
             d.flags = ipc.open(*pi["flags"])
             d.rank, d.slot = p, pi["neigh"].index(r)
+        # piece i of ours receives what the peer sends in ITS k-th piece
+        # toward us, k = i's rank among our pieces from that peer counted in
+        # reverse order (the RCCL transport's matching, _recv_match)
         row_src = (ctypes.c_longlong * max(1, len(rows)))()
         for i, x in enumerate(rows):
-            mine = [y for y in by_rank[x[0]]["rows"] if y[0] == r]
-            if len(mine) != 1 or mine[0][3] != x[3]:
+            pr = by_rank[x[0]]["rows"]
+            m = _recv_match(rows, i, pr, r)
+            if m < 0 or pr[m][3] != x[3]:
                 raise RuntimeError(f"rank {r}: inconsistent row halo plan with rank {x[0]}")
-            row_src[i] = mine[0][1]
+            row_src[i] = pr[m][1]
         blk_src = (ctypes.c_longlong * max(1, len(cols)))()
         for i, c in enumerate(cols):
             pc = by_rank[c[0]]["cols"]
-            m = [k for k, y in enumerate(pc) if y[0] == r]
-            if len(m) != 1 or pc[m[0]][5:7] != c[5:7]:
+            m = _recv_match(cols, i, pc, r)
+            if m < 0 or list(pc[m][5:7]) != list(c[5:7]):
                 raise RuntimeError(f"rank {r}: inconsistent block halo plan with rank {c[0]}")
-            blk_src[i] = sum(y[5] * y[6] for y in pc[:m[0]])
+            blk_src[i] = sum(y[5] * y[6] for y in pc[:m])
         epoch = ctypes.c_longlong(0)
         plan.flags = flags.data_ptr()
         plan.timeout = flags.data_ptr() + 4 * _IPC_TIMEOUT_WORD
@@ -602,7 +656,116 @@ class DistHeat:
             return "stream2" + suffix
         return ("pipe" if self.kernel == "pipe" else "stream") + str(self.tblock) + suffix
 
+    # -- native loop selection (run) ------------------------------------
+    def enable_native(self, transport: str | None = None, fused: bool = True) -> dict:
+        """One-time, collective setup of the native loop that :meth:`run`
+        uses on the GPU (``native="auto"`` / ``"on"``). Picks the transport
+        -- loopback when every subdomain is in this process, RCCL over an
+        ``nccl`` group, IPC-mapped peers over a ``gloo`` group on the GPU (the
+        shared-GPU rehearsal) or as ``transport`` says -- then checks the
+        native loop bit for bit against the Python loop on a small problem of
+        the same decomposition (:func:`native_selftest`): first with the
+        fused one-launch schedule, then (if that fails) schedule 0. Every
+        rank agrees on each step, so no rank is left alone in a collective.
+        With ``"auto"`` a failure leaves :meth:`run` on the Python loop;
+        with ``"on"`` it raises. Returns :attr:`native_info`."""
+        if self.native_info is not None:
+            return self.native_info
+        info = {"loop": "python", "transport": None, "fused_allowed": False, "selftest": None, "schedule": None}
+        self.native_info = info
+        if self.native_mode == "off" or self.device.type != "cuda" or self.solo():
+            return info
+        from .. import _ext
+
+        def agree(ok: bool) -> bool:
+            t = torch.tensor([1.0 if ok else 0.0], device=self.device)
+            self.comm.allreduce_(t, "min")
+            return bool(t.item() == 1.0)
+
+        try:
+            _ext.hip()
+            ok = True
+        except Exception as e:  # noqa: BLE001 - reported; every rank falls back together
+            print(f"DistHeat rank {self.comm.rank}: native library unavailable ({e})", flush=True)
+            ok = False
+        handle, kind = None, "loopback"
+        # RCCL may be asked for at world 1 too (a periodic grid's halos are
+        # then self-sends); IPC needs other processes to map
+        if agree(ok) and (self.comm.size > 1 or transport == "rccl"):
+            backend = getattr(self.comm, "backend", None)
+            kind = transport or ("rccl" if backend == "nccl" else "ipc")
+            try:
+                if kind == "rccl":
+                    from ..parallel.rccl import NativeRccl
+
+                    handle = NativeRccl(getattr(self.comm, "group", None))
+                else:
+                    from ..parallel.ipc import NativeIpc
+
+                    handle = NativeIpc(getattr(self.comm, "group", None))
+            except Exception as e:  # noqa: BLE001
+                print(f"DistHeat rank {self.comm.rank}: native {kind} transport unavailable ({e})", flush=True)
+                ok = False
+            ok = agree(ok)
+        elif not ok:
+            ok = False
+        if ok:
+            ok = False
+            for f in ((True, False) if fused else (False,)):
+                try:
+                    good = native_selftest(self, kind, handle, f)
+                except Exception as e:  # noqa: BLE001 - e.g. the gated grid refused, a timed-out wait
+                    print(f"DistHeat rank {self.comm.rank}: native self-test raised ({e})", flush=True)
+                    good = False
+                if agree(good):
+                    ok, fused = True, f
+                    break
+        if not ok:
+            if handle is not None and kind == "rccl":
+                handle.abort()  # pending native sends/recvs fail on the peers instead of hanging
+            if self.native_mode == "on":
+                raise RuntimeError("native distributed loop failed its setup or bitwise self-test")
+            return info
+        self._native = (kind, handle)
+        info.update(loop="native", transport=kind, fused_allowed=fused, selftest=True)
+        return info
+
+    def _run_native_selected(self, iters: int, sync: bool | None) -> None:
+        kind, handle = self._native
+        fused = self.native_info["fused_allowed"]
+        if kind == "rccl":
+            self.run_native(iters, handle, sync=sync, fused=fused)
+        elif kind == "ipc":
+            self.run_native(iters, ipc=handle, sync=sync, fused=fused)
+        else:
+            self.run_native(iters, sync=sync, fused=fused)
+        self.native_info["schedule"] = self.schedule()["schedule"]
+
+    def check_native(self) -> None:
+        """After the caller's final sync: raise if the native loop's bounded
+        in-kernel waits gave up (fused border gate, IPC epochs) or RCCL
+        reported an asynchronous error. The sticky words live in pinned host
+        memory, so this costs one device sync."""
+        kind, handle = getattr(self, "_native", (None, None))
+        self.gate_check()
+        if kind == "ipc":
+            self.ipc_check()
+        elif kind == "rccl":
+            handle.check()
+
+    def close_native(self) -> None:
+        """Release the native transport (collective for IPC)."""
+        kind, handle = getattr(self, "_native", (None, None))
+        self._native = (None, None)
+        if handle is not None:
+            handle.close()
+
     def run(self, iters: int, sync: bool | None = None) -> None:
+        """``iters`` timesteps. One GPU subdomain with no neighbour: one
+        native multi-pass call. Otherwise, on the GPU with ``native="auto"``
+        / ``"on"``: the native C++ loop (after :meth:`enable_native`'s
+        self-test), whose in-kernel waits are checked -- and raise -- at the
+        end of every call; else the Python loop below (any backend)."""
         if self.solo():
             self.finish()
             s = next(iter(self.subs.values()))
@@ -613,6 +776,11 @@ class DistHeat:
             g.iteration += iters
             self.iteration += iters
             return
+        if self.native_mode != "off" and self.device.type == "cuda" and iters > 0:
+            if self.enable_native()["loop"] == "native":
+                self._run_native_selected(iters, sync)
+                self.check_native()
+                return
         i = 0
         while iters - i >= 2 and self.tblock >= 2:
             ns = min(self.tblock, iters - i)
@@ -635,17 +803,18 @@ class DistHeat:
         has no restart path, only lossy text dumps."""
         import os
 
-        from ..utils.gridio import save_checkpoint
-
         self.finish()
         os.makedirs(directory, exist_ok=True)
+        prev = _ACTIVE_WRITERS.get(os.path.realpath(directory))
+        if prev is not None:
+            prev._thread.join()  # an asynchronous checkpoint into the same files is still writing
         paths = []
         for r, s in self.subs.items():
             g = s.grid
             H = g.H
             own = g.buf[g.cur, H:H + g.ny, H:H + g.nx].cpu().numpy()
             path = os.path.join(directory, f"heat_rank{r}.safetensors")
-            save_checkpoint(path, {"interior": own}, self._meta(r))
+            _save_atomic(path, {"interior": own}, self._meta(r))
             paths.append(path)
         return paths
 
@@ -730,6 +899,72 @@ class DistHeat:
         return out
 
 
+def native_selftest(sim: "DistHeat", kind: str, handle, fused: bool, n: int = 1024) -> bool:
+    """Bitwise self-test of the native loop for ``sim``'s decomposition and
+    pass schedule (collective). A problem of at most ``n``^2 points with the
+    same world, method, periodicity, dtype, steps per pass, kernel and FMA
+    mode, and a non-uniform interior (a stale or misplaced halo changes the
+    answer), runs ``2*tblock + 1`` steps (whole passes plus a tail) through
+    the native loop on transport ``kind`` and through the Python loop's
+    single steps; True on this rank if they agree bit for bit and no
+    in-kernel wait gave up. A native run that does not finish in 60 s
+    fails."""
+    p0 = sim.p
+    iters = 2 * sim.tblock + 1
+    p = SimParams(nx=min(p0.nx, n), ny=min(p0.ny, n), iters=iters, order=p0.order, ic=5.0,
+                  bc=(0.0, 10.0, 3.0, 7.0), grid_method=p0.grid_method, sync=p0.sync, flavor="hw5")
+    dt = next(iter(sim.subs.values())).grid.dtype
+    kw = dict(local_ranks=list(sim.local_ranks), world=sim.world, periodic=sim.periodic, fma=sim.fma)
+    a = DistHeat(p, sim.comm, dt, sim.device, tblock=sim.tblock, kernel=sim.kernel, **kw)
+    b = DistHeat(p, sim.comm, dt, sim.device, tblock=1, **kw)
+    for d in (a, b):
+        for s in d.subs.values():
+            g, H = s.grid, s.grid.H
+            yy = torch.arange(s.blk.ny, device=sim.device, dtype=dt).view(-1, 1) + s.blk.y0
+            xx = torch.arange(s.blk.nx, device=sim.device, dtype=dt).view(1, -1) + s.blk.x0
+            g.buf[:, H:H + s.blk.ny, H:H + s.blk.nx] = 5.0 + torch.sin(0.05 * xx) * torch.cos(0.03 * yy)
+        d.exchange(d._cur()).wait()
+    if kind == "rccl":
+        a.run_native(iters, handle, fused=fused)
+    elif kind == "ipc":
+        a.run_native(iters, ipc=handle, fused=fused)
+    else:
+        a.run_native(iters, fused=fused)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(sim.device))
+    t_end = time.perf_counter() + 60.0
+    while not ev.query():
+        if time.perf_counter() > t_end:
+            raise TimeoutError("native self-test run did not finish within 60 s")
+        time.sleep(0.002)
+    a.gate_check()
+    if kind == "ipc":
+        a.ipc_check()
+    b.run(iters)
+    torch.cuda.synchronize(sim.device)
+    def own(s):
+        g, H = s.grid, s.grid.H
+        return g.buf[g.cur, H:H + g.ny, H:H + g.nx]
+
+    same = all(torch.equal(own(sa), own(sb)) for sa, sb in zip(a.subs.values(), b.subs.values()))
+    if kind == "ipc":
+        # a's plan mapped the peers' test grids; drop those mappings before
+        # the test solvers' memory is freed (collective)
+        handle.close()
+    return same
+
+
+def _recv_match(mine: list, i: int, theirs: list, me: int) -> int:
+    """Index in the peer's piece list ``theirs`` of the send that our piece
+    ``i`` receives: receives are posted in reverse order, sends in forward
+    order, so the k-th receive from a peer (counting our pieces i+1.. from
+    it first) pairs with its k-th send to ``me``. -1 if there is none."""
+    peer = mine[i][0]
+    k = sum(1 for x in mine[i + 1:] if x[0] == peer)
+    idx = [j for j, y in enumerate(theirs) if y[0] == me]
+    return idx[k] if k < len(idx) else -1
+
+
 def _inner_box(s: _Sub, depth: int):
     """Owned region shrunk by ``depth`` on every side that has a neighbour."""
     g, b = s.grid, s.blk
@@ -781,20 +1016,33 @@ def _ext_region(s: _Sub):
 
 
 def run_hw5(params_path: str, comm: Comm | None = None, dtype=torch.float64, device: str | None = None,
-            write_files: bool = True, tblock: int | str = "auto", fma: bool = False, kernel: str = "auto") -> dict:
+            write_files: bool = True, tblock: int | str = "auto", fma: bool = False, kernel: str = "auto",
+            native: str = "auto", local_ranks: list[int] | None = None, world: int | None = None,
+            periodic: tuple[bool, bool] = (False, False), transport: str | None = None) -> dict:
     """The hw5 driver (double precision, as the reference). On the GPU the
     steps per pass and the pass kernel are chosen from the subdomain size
     (:func:`auto_tblock`, :func:`auto_kernel`); ``fma=False`` keeps the
-    reference CPU's uncontracted arithmetic."""
+    reference CPU's uncontracted arithmetic. With neighbours on the GPU the
+    time loop is the native C++ loop (``native="auto"``: after its bitwise
+    self-test, else the Python loop; rank 0 logs which); an in-kernel wait
+    that gave up raises ``RuntimeError`` after the run.
+    ``local_ranks``/``world``: several subdomains in this process
+    (``heat2d_mpi --ranks N``)."""
     comm = comm or LoopbackComm()
     p = SimParams.from_file(params_path, flavor="hw5")
     if comm.rank == 0:
         print(p.banner())
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
-    sim = DistHeat(p, comm, dtype, device, tblock=tblock, fma=fma, kernel=kernel)
+    sim = DistHeat(p, comm, dtype, device, tblock=tblock, fma=fma, kernel=kernel, native=native,
+                   local_ranks=local_ranks, world=world, periodic=periodic)
     if write_files:
         sim.save_text("init")
     if sim.device.type == "cuda":
+        info = sim.enable_native(transport)
+        if comm.rank == 0 and not sim.solo():
+            print(f"time loop: {info['loop']}" + (f" ({info['transport']} transport, bitwise self-test passed, "
+                                                   f"fused schedule {'allowed' if info['fused_allowed'] else 'off'})"
+                                                   if info["loop"] == "native" else ""), flush=True)
         torch.cuda.synchronize()
     comm.barrier()
     t0 = time.perf_counter()
@@ -805,6 +1053,8 @@ def run_hw5(params_path: str, comm: Comm | None = None, dtype=torch.float64, dev
     secs = time.perf_counter() - t0
     if comm.rank == 0:
         print(f"{p.iters} iterations on a {p.nx} by {p.ny} grid took: {secs} seconds.")
+        if sim.native_info and sim.native_info.get("schedule"):
+            print(f"native schedule: {sim.native_info['schedule']}", flush=True)
     if write_files:
         sim.save_text("final")
     return {"seconds": secs, "sim": sim}

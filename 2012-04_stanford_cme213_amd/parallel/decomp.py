@@ -47,12 +47,17 @@ class Block:
     right: int = -1
     top: int = -1
     bottom: int = -1
+    periodic: tuple[bool, bool] = (False, False)
 
     def neighbor(self, dx: int, dy: int) -> int:
         """Rank of the block at (col + dx, row + dy), or -1 outside the grid
-        (dy = +1 is "top"). Diagonal peers feed the corner halos that
-        temporal blocking needs."""
+        (dy = +1 is "top"); periodic axes wrap. Diagonal peers feed the
+        corner halos that temporal blocking needs."""
         c, r = self.col + dx, self.row + dy
+        if self.periodic[0]:
+            c %= self.px
+        if self.periodic[1]:
+            r %= self.py
         if 0 <= c < self.px and 0 <= r < self.py:
             return r * self.px + c
         return -1
@@ -63,18 +68,13 @@ class Block:
         return (self.top < 0, self.left < 0, self.bottom < 0, self.right < 0)
 
 
-def decompose(nx: int, ny: int, P: int, method: int, rank: int) -> Block:
+def decompose(nx: int, ny: int, P: int, method: int, rank: int,
+              periodic: tuple[bool, bool] = (False, False)) -> Block:
     Px, Py = proc_grid(P, method)
     row, col = divmod(rank, Px)
     x0, lnx = _split(nx, Px, col)
     y0, lny = _split(ny, Py, row)
-    b = Block(rank, Px, Py, col, row, x0, y0, lnx, lny)
-    if row > 0:
-        b.bottom = (row - 1) * Px + col
-    if row < Py - 1:
-        b.top = (row + 1) * Px + col
-    if col > 0:
-        b.left = rank - 1
-    if col < Px - 1:
-        b.right = rank + 1
+    b = Block(rank, Px, Py, col, row, x0, y0, lnx, lny, periodic=(bool(periodic[0]), bool(periodic[1])))
+    b.bottom, b.top = b.neighbor(0, -1), b.neighbor(0, 1)
+    b.left, b.right = b.neighbor(-1, 0), b.neighbor(1, 0)
     return b

@@ -35,31 +35,13 @@ sys.path.insert(0, REPO)
 BASELINE_GBPS = 239.7  # heat 4000^2 order 8 LDS kernel, 48.07 ms / 10 iters, 72 B/pt
 
 
-def _wait_bounded(dev, seconds: float) -> bool:
-    """Wait for the work queued on the current stream, giving up after
-    ``seconds`` (a hung exchange must not hang the bench)."""
-    import torch
-
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(dev))
-    t_end = time.perf_counter() + seconds
-    while not ev.query():
-        if time.perf_counter() > t_end:
-            return False
-        time.sleep(0.005)
-    return True
-
-
-def selftest(comm, native, dev, args, fused: bool = True) -> bool:
-    """Bitwise self-test of the timed path. A 1024^2 problem with a
-    non-uniform interior runs 2*tblock+1 timesteps (whole passes plus a tail)
-    along the EXACT path the timed loop takes -- the native multi-pass driver
-    at N = 1, the native loop (RCCL or IPC transport; ``fused`` = whether the
-    fused schedule may be used) at N > 1 -- and must equal, bit for bit on
-    every rank, the same number of single FMA steps of the torch.distributed
-    loop (the path the multi-process CPU tests cover). A native run that does
-    not finish within 60 s counts as a failure (the caller aborts the
-    communicator)."""
+def selftest(comm, dev, args) -> bool:
+    """Bitwise self-test of the N = 1 timed path (the native multi-pass
+    driver, ``heat_run``): a 1024^2 problem with a non-uniform interior runs
+    2*tblock+1 timesteps (whole passes plus a tail) and must equal, bit for
+    bit, the same number of single FMA steps. (N > 1: the solver's own
+    :meth:`DistHeat.enable_native` self-test of the native loop against the
+    torch.distributed loop.)"""
     import torch
 
     from cme213x.models.heat2d_dist import DistHeat
@@ -71,7 +53,7 @@ def selftest(comm, native, dev, args, fused: bool = True) -> bool:
     a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma),
                  kernel=args.kernel)
     b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1, fma=bool(args.fma))
-    # non-uniform interior so a stale or misplaced halo changes the answer
+    # non-uniform interior so a misplaced pass boundary changes the answer
     for sim in (a, b):
         s = next(iter(sim.subs.values()))
         g, B = s.grid, s.grid.H
@@ -79,18 +61,7 @@ def selftest(comm, native, dev, args, fused: bool = True) -> bool:
         xx = torch.arange(s.blk.nx, device=dev, dtype=torch.float32).view(1, -1) + s.blk.x0
         g.buf[:, B:B + s.blk.ny, B:B + s.blk.nx] = 5.0 + torch.sin(0.05 * xx) * torch.cos(0.03 * yy)
         sim.exchange(sim._cur()).wait()
-    if native is None:
-        a.run(iters)
-    elif args.transport == "ipc":
-        a.run_native(iters, ipc=native, fused=fused)
-    else:
-        a.run_native(iters, native, fused=fused)
-    if not _wait_bounded(dev, 60.0):
-        raise TimeoutError("self-test run did not finish within 60 s")
-    if native is not None:
-        if args.transport == "ipc":
-            a.ipc_check()
-        a.gate_check()  # fused schedule: no border wait gave up on the exchange
+    a.run(iters)
     for _ in range(iters):
         b.step()
     b.finish()
@@ -98,9 +69,7 @@ def selftest(comm, native, dev, args, fused: bool = True) -> bool:
     sa, sb = next(iter(a.subs.values())).grid, next(iter(b.subs.values())).grid
     B = sa.B
     va, vb = sa.view()[B:B + sa.ny, B:B + sa.nx], sb.view()[B:B + sb.ny, B:B + sb.nx]
-    bad = torch.tensor([0.0 if torch.equal(va, vb) else 1.0], device=dev)
-    comm.allreduce_(bad, "max")
-    return bool(bad.item() == 0)
+    return bool(torch.equal(va, vb))
 
 
 def auto_tblock(points_per_rank: int, kernel: str = "pipe") -> int:
@@ -151,6 +120,9 @@ def main() -> int:
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
                          "(tests; never the reported number)")
+    ap.add_argument("--ic", choices=["uniform", "random", "both"], default="both",
+                    help="uniform: the reference's IC 5.0 only (the headline value); both: also time the same K "
+                         "steps from a random-init field (ms_per_step_random)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0 with a gloo control plane and the IPC transport "
                          "(exercises the multi-rank flow on a 1-GPU box; the number is not a scaling result)")
@@ -161,7 +133,7 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    import cme213x
+    import cme213x  # noqa: F401 - the package alias
     from cme213x.models.heat2d import bytes_per_point
     from cme213x.models.heat2d_dist import DistHeat
     from cme213x.parallel.comm import init_from_env
@@ -186,79 +158,31 @@ def main() -> int:
     p = SimParams(nx=args.n, ny=args.n, iters=args.steps, order=args.order, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
-    def agree(ok: bool) -> bool:
-        t = torch.tensor([1.0 if ok else 0.0], device=dev)
-        comm.allreduce_(t, "min")
-        return bool(t.item() == 1.0)
-
-    native, native_ok = None, False
-    fused = args.schedule == "auto"
-    if on_gpu and comm.size > 1 and args.native != "off":
-        # 1) every rank can load the native library -- agreed BEFORE any
-        #    collective native setup, so no rank is left alone inside
-        #    ncclCommInitRank / the IPC handle exchange
-        try:
-            cme213x._ext.hip()
-            lib_ok = True
-        except Exception as e:  # noqa: BLE001
-            print(f"bench.py rank {rank}: native library unavailable ({e})", file=sys.stderr)
-            lib_ok = False
-        native_ok = agree(lib_ok)
-        # 2) collective setup + bitwise self-test; any failure (or a hang,
-        #    bounded at 60 s) on any rank makes every rank fall back together
-        if native_ok:
-            try:
-                if args.transport == "ipc":
-                    from cme213x.parallel.ipc import NativeIpc
-
-                    native = NativeIpc()
-                else:
-                    from cme213x.parallel.rccl import NativeRccl
-
-                    native = NativeRccl()
-                if args.native == "auto":
-                    try:
-                        native_ok = selftest(comm, native, dev, args, fused=fused)
-                    except Exception as e:  # noqa: BLE001 - e.g. the fused launch refused its gated grid
-                        print(f"bench.py rank {rank}: native self-test raised ({e})", file=sys.stderr)
-                        native_ok = False
-                    if not agree(native_ok) and fused:
-                        # the fused gated schedule failed (or its probe refused
-                        # it on some rank): retry the native loop on schedule 0
-                        print(f"bench.py rank {rank}: fused native schedule failed the self-test; "
-                              "retrying with schedule 0", file=sys.stderr)
-                        fused = False
-                        native_ok = selftest(comm, native, dev, args, fused=False)
-                else:
-                    native_ok = True
-            except Exception as e:  # noqa: BLE001 - reported, then the portable path runs
-                print(f"bench.py rank {rank}: native {args.transport} loop unavailable ({e}); "
-                      "using torch.distributed", file=sys.stderr)
-                native_ok = False
-                if native is not None and args.transport == "rccl":
-                    native.abort()  # pending native sends/recvs fail on the peers instead of hanging
-            native_ok = agree(native_ok)
-        if not native_ok and (args.native == "on" or args.share_gpu):
-            print("bench.py: --native on but the native loop failed", file=sys.stderr)
-            return 3
-    use_native = native is not None and native_ok
-
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
-                   fma=bool(args.fma), kernel=args.kernel)
+                   fma=bool(args.fma), kernel=args.kernel,
+                   native=("off" if (not on_gpu or comm.size == 1) else args.native))
+    # N > 1: the solver's own native-loop setup -- transport, then a bitwise
+    # self-test against the torch.distributed loop (fused schedule first,
+    # schedule 0 if that fails); every rank agrees, "auto" falls back to the
+    # torch.distributed loop, "on" raises
+    try:
+        info = sim.enable_native(args.transport if not args.share_gpu else "ipc", fused=args.schedule == "auto")
+    except RuntimeError as e:
+        print(f"bench.py: --native on but the native loop failed ({e})", file=sys.stderr)
+        return 3
+    if args.share_gpu and info["loop"] != "native":
+        print("bench.py: --share-gpu needs the native IPC loop, which failed", file=sys.stderr)
+        return 3
+    use_native = info["loop"] == "native"
     init_state = {(s.blk.x0, s.blk.y0): s.grid.buf.clone() for s in sim.subs.values()} if on_gpu else {}
 
     def run(k):
-        if use_native and args.transport == "ipc":
-            sim.run_native(k, ipc=native, fused=fused)
-        elif use_native:
-            sim.run_native(k, native, fused=fused)
-        else:
-            sim.run(k)
+        sim.run(k)
 
-    # the timed path's bitwise self-test at N = 1 (N > 1: above, per transport)
-    selftest_ok = native_ok if use_native else None
+    # the timed path's bitwise self-test at N = 1 (N > 1: enable_native above)
+    selftest_ok = info["selftest"] if use_native else None
     if on_gpu and comm.size == 1:
-        selftest_ok = selftest(comm, None, dev, args)
+        selftest_ok = selftest(comm, dev, args)
 
     def barrier_sync():
         sync()
@@ -290,28 +214,63 @@ def main() -> int:
             s.grid.buf.copy_(init_state[(s.blk.x0, s.blk.y0)])
             s.grid.iteration = 0
         sim.iteration = 0
-    run(args.warmup)
-    barrier_sync()
-    t0 = time.perf_counter()
-    run(args.steps)
-    sync()
-    t1 = time.perf_counter()
-    comm.barrier()
-    if use_native and args.transport == "rccl":
-        native.check()  # surface asynchronous RCCL failures instead of reporting a number
-    elif use_native:
-        sim.ipc_check()  # a wait that gave up on a peer invalidates the run
-    if use_native:
-        sim.gate_check()  # ... as does a fused-schedule border wait that gave up
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    comm.allreduce_(elapsed, "max")
-    secs = float(elapsed.item())
 
-    # sanity: the solution must stay finite and within the BC/IC bounds
-    local = next(iter(sim.subs.values())).grid
-    st = local.buf[local.cur]
-    bad = torch.tensor([float(~torch.isfinite(st).all()) + float(st.abs().max() > 1e3)], device=dev)
-    comm.allreduce_(bad, "max")
+    def timed(k):
+        """W warmup steps, then exactly k timed steps between barrier +
+        synchronize; max over ranks (s). The native loop checks its in-kernel
+        waits (and RCCL's asynchronous errors) at the end of every run and
+        raises instead of reporting a number."""
+        run(args.warmup)
+        barrier_sync()
+        t0 = time.perf_counter()
+        run(k)
+        sync()
+        t1 = time.perf_counter()
+        comm.barrier()
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        comm.allreduce_(elapsed, "max")
+        return float(elapsed.item())
+
+    def sane() -> bool:
+        """the solution must stay finite and within the BC/IC bounds"""
+        local = next(iter(sim.subs.values())).grid
+        st = local.buf[local.cur]
+        bad = torch.tensor([float(~torch.isfinite(st).all()) + float(st.abs().max() > 1e3)], device=dev)
+        comm.allreduce_(bad, "max")
+        return bool(bad.item() == 0)
+
+    secs = timed(args.steps)
+    sanity_ok = sane()
+
+    # the same K steps from a random-init field (BASELINE.json: "synthetic
+    # random-init inputs"): uniform(0, 10) interior, seeded per rank, same
+    # BCs. The pass is issue/power bound, and random data toggles more bits
+    # than the reference's uniform IC, so this is the slower figure.
+    secs_random = None
+    if on_gpu and args.ic in ("both", "random"):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
+        for s in sim.subs.values():
+            g, H = s.grid, s.grid.H
+            g.buf[:, H:H + g.ny, H:H + g.nx] = torch.rand((g.ny, g.nx), generator=gen, device=dev) * 10.0
+        sim.exchange(sim._cur()).wait()
+        sync()
+        secs_random = timed(args.steps)
+        sanity_ok = sanity_ok and sane()
+
+    # N = 1: the distributed native schedule (cme_heat_dist_run, the loop the
+    # N > 1 points run, exchange off) on the same grid, so the N = 1 point of
+    # a scaling curve can be read against the same schedule
+    secs_dist1 = None
+    if on_gpu and comm.size == 1 and args.kernel == "pipe":
+        run_d = lambda k: sim.run_native(k, transport=2)  # noqa: E731
+        run_d(args.warmup)
+        sync()
+        t0 = time.perf_counter()
+        run_d(args.steps)
+        sync()
+        secs_dist1 = time.perf_counter() - t0
+        sim.gate_check()
 
     if use_native:
         sch = DistHeat.schedule()
@@ -355,22 +314,28 @@ def main() -> int:
                 "tblock": args.tblock,
                 "device": args.device,
                 "rehearsal_shared_gpu": bool(args.share_gpu),
-                "loop": f"native-{args.transport}" if use_native else ("torch.distributed" if comm.size > 1
-                                                                         else "single (native multi-pass)"),
-                "transport": (args.transport if use_native else ("torch.distributed" if comm.size > 1 else "none")),
+                "loop": f"native-{info['transport']}" if use_native else ("torch.distributed" if comm.size > 1
+                                                                            else "single (native multi-pass)"),
+                "transport": (info["transport"] if use_native else ("torch.distributed" if comm.size > 1 else "none")),
                 "schedule": schedule,
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
             "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),
             "gpoints_per_s": round(pts * args.steps / secs / 1e9, 2),
-            "sanity_ok": bool(bad.item() == 0),
+            # a failed bitwise self-test of the timed path invalidates the record
+            "sanity_ok": bool(sanity_ok and selftest_ok is not False),
             "selftest": selftest_ok,
-            "native_selftest": (native_ok if native is not None else None),
+            "native_selftest": (info["selftest"] if comm.size > 1 and on_gpu else None),
             "spinup_steps": spin,
         }
+        if secs_random is not None:
+            rec["ms_per_step_random"] = round(secs_random * 1e3 / args.steps, 4)
+            rec["value_random"] = round(pts * bpp * args.steps / secs_random / 1e9, 2)
+            rec["data_random"] = "synthetic random-init interior, uniform(0, 10), seed 1234 + rank, same BCs"
+        if secs_dist1 is not None:
+            rec["ms_per_step_dist_schedule"] = round(secs_dist1 * 1e3 / args.steps, 4)
         print(json.dumps(rec), flush=True)
-    if use_native and args.transport == "ipc":
-        native.close()
+    sim.close_native()
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

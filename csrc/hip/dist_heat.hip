@@ -652,17 +652,28 @@ int post_exchange_rccl(ncclComm_t comm, const SubDesc& d, T* g, ncclDataType_t d
     if (d.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
     const long long total = stage_layout(d, off);
     CME_TRY_INT(pack_blocks<T>(d, g, cs));
+    // Sends in plan order, receives in REVERSE plan order (rows, then
+    // blocks). The plan lists rows top, bottom and blocks left, corners,
+    // right -- piece i and piece n-1-i of a group face opposite ways -- so a
+    // peer's k-th send to us meets our k-th receive from it even when one
+    // peer sits on several sides (periodic grids; with one block per axis
+    // that peer is this rank itself, and RCCL moves the bytes as self-sends).
     NCCL_TRY(ncclGroupStart());
     for (int i = 0; i < d.n_rows; ++i) {
         const long long* r = d.rows + i * 4;
         NCCL_TRY(ncclSend(g + r[1], (size_t)r[3], dt, (int)r[0], comm, cs));
-        NCCL_TRY(ncclRecv(g + r[2], (size_t)r[3], dt, (int)r[0], comm, cs));
     }
     for (int i = 0; i < d.n_blks; ++i) {
         const int* c = d.blks + i * kBlk;
-        const long long cnt = (long long)c[5] * c[6];
-        NCCL_TRY(ncclSend(stage + off[i], (size_t)cnt, dt, c[0], comm, cs));
-        NCCL_TRY(ncclRecv(stage + total + off[i], (size_t)cnt, dt, c[0], comm, cs));
+        NCCL_TRY(ncclSend(stage + off[i], (size_t)((long long)c[5] * c[6]), dt, c[0], comm, cs));
+    }
+    for (int i = d.n_rows - 1; i >= 0; --i) {
+        const long long* r = d.rows + i * 4;
+        NCCL_TRY(ncclRecv(g + r[2], (size_t)r[3], dt, (int)r[0], comm, cs));
+    }
+    for (int i = d.n_blks - 1; i >= 0; --i) {
+        const int* c = d.blks + i * kBlk;
+        NCCL_TRY(ncclRecv(stage + total + off[i], (size_t)((long long)c[5] * c[6]), dt, c[0], comm, cs));
     }
     NCCL_TRY(ncclGroupEnd());
     return unpack_blocks<T>(d, g, cs);
@@ -671,6 +682,20 @@ int post_exchange_rccl(ncclComm_t comm, const SubDesc& d, T* g, ncclDataType_t d
 int find_sub(const SubDesc* subs, int nsub, int rank) {
     for (int i = 0; i < nsub; ++i)
         if (subs[i].rank == rank) return i;
+    return -1;
+}
+
+// The RCCL transport's matching, for the transports that pull: our piece i
+// (of n, peer at stride*j) is the k-th receive from that peer in reverse
+// order, k = pieces after i with the same peer; it reads the peer's k-th
+// piece toward `me` in forward order. Returns that index, or -1.
+template <typename I>
+int recv_match(const I* mine, int n, int i, const I* theirs, int tn, int stride, int me) {
+    const I peer = mine[i * stride];
+    int k = 0;
+    for (int j = i + 1; j < n; ++j) k += mine[j * stride] == peer;
+    for (int j = 0; j < tn; ++j)
+        if (theirs[j * stride] == (I)me && k-- == 0) return j;
     return -1;
 }
 
@@ -689,11 +714,9 @@ int pull_loopback(const SubDesc* subs, int nsub, int si, int k, hipStream_t cs) 
         const int pj = find_sub(subs, nsub, (int)r[0]);
         if (pj < 0 || l.n >= kMaxSegs) return (int)hipErrorInvalidValue;
         const SubDesc& pd = subs[pj];
-        long long src_off = -1;
-        for (int j = 0; j < pd.n_rows; ++j)
-            if (pd.rows[j * 4] == d.rank) src_off = pd.rows[j * 4 + 1];
-        if (src_off < 0) return (int)hipErrorInvalidValue;
-        l.src[l.n] = (const T*)pd.buf[k] + src_off;
+        const int m = recv_match<long long>(d.rows, d.n_rows, i, pd.rows, pd.n_rows, 4, d.rank);
+        if (m < 0 || pd.rows[m * 4 + 3] != r[3]) return (int)hipErrorInvalidValue;
+        l.src[l.n] = (const T*)pd.buf[k] + pd.rows[m * 4 + 1];
         l.dst[l.n] = g + r[2];
         l.bytes[l.n++] = r[3] * (long long)sizeof(T);
     }
@@ -707,9 +730,7 @@ int pull_loopback(const SubDesc* subs, int nsub, int si, int k, hipStream_t cs) 
         const SubDesc& pd = subs[pj];
         if (pd.n_blks > kMaxPieces) return (int)hipErrorInvalidValue;
         stage_layout(pd, poff);
-        int m = -1;
-        for (int j = 0; j < pd.n_blks; ++j)
-            if (pd.blks[j * kBlk] == d.rank) m = j;
+        const int m = recv_match<int>(d.blks, d.n_blks, i, pd.blks, pd.n_blks, kBlk, d.rank);
         if (m < 0 || pd.blks[m * kBlk + 5] != c[5] || pd.blks[m * kBlk + 6] != c[6]) return (int)hipErrorInvalidValue;
         l.src[l.n] = (const T*)pd.stage + poff[m];
         l.dst[l.n] = (T*)d.stage + total + off[i];
@@ -866,8 +887,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     //  * the queue-independence probe passed (run_gate_probe).
     // Other configurations use schedule 0.
     bool fused = schedule == 2 && !(fma & kNoFused) && !sync && nsub == 1 && (fma & kKernelPipe) &&
-                 tblock >= 3 && transport != 1 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions &&
-                 subs[0].n_int >= 1;
+                 tblock >= 3 && subs[0].n_int + subs[0].n_b <= cme::kMaxS2Regions && subs[0].n_int >= 1;
     DistCtx* ctx;
     CME_TRY_INT(get_ctx(nsub, &ctx));
     if (fused) {
@@ -884,17 +904,24 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
         if (transport == 1 && npeer[si] != subs[si].n_rows + subs[si].n_blks) return (int)hipErrorInvalidValue;
     }
     long long epoch = (transport == 3) ? *subs[0].ipc->epoch : 0;
+    // CME_DIST_FAKE_XCHG_US (read per call): transport 2 stands a delay in
+    // for the network between real pack / unpack kernels (rehearsal timing,
+    // benchmarks/bench_dist_rank.py); the other transports hold their comm
+    // stream that long before each exchange (a test forces the fused gate's
+    // timeout path this way)
+    const int fake_us = [] {
+        const char* e = getenv("CME_DIST_FAKE_XCHG_US");
+        return e ? atoi(e) : 0;
+    }();
     // Exchange the halos of state k for every sub. The caller has made each
     // comm stream wait for what the exchange reads; ev_comm is recorded after.
     auto exchange_all = [&](int k) -> int {
+        if (transport != 2 && fake_us > 0)
+            for (int si = 0; si < nsub; ++si) CME_TRY_INT(launch_delay_us(fake_us, ctx->sub[si].comm));
         if (transport == 0)
             return post_exchange_rccl<T>(comm, subs[0], (T*)subs[0].buf[k], dt, ctx->sub[0].comm);
         if (transport == 3) return post_exchange_ipc<T>(subs[0], k, (unsigned)(++epoch), ctx->sub[0].comm);
         if (transport == 2) {
-            static const int fake_us = [] {
-                const char* e = getenv("CME_DIST_FAKE_XCHG_US");
-                return e ? atoi(e) : 0;
-            }();
             if (fake_us <= 0) return 0;
             for (int si = 0; si < nsub; ++si) {  // pack -> "network" -> unpack, as transport 0
                 SubCtx& u = ctx->sub[si];

@@ -415,7 +415,7 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
             for (unsigned spins = 0;; ++spins) {
                 const unsigned v = __hip_atomic_load(gate.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((int)(v - gate.val) >= 0) break;
-                if (spins >= (1u << 24)) {
+                if (spins >= gate.spins) {
                     __hip_atomic_store(gate.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }

@@ -45,6 +45,14 @@ int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n
         default: return (int)hipErrorInvalidValue;
     }
 }
+// poll bound of the fused schedule's gated border workgroups (PipeGate):
+// CME_DIST_GATE_SPINS, read per call (a test forces the timeout path in-process)
+unsigned gate_spin_limit() {
+    const char* e = getenv("CME_DIST_GATE_SPINS");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (unsigned)v : (1u << 24);
+}
+
 template <bool FMA>
 int pipe_order(int order, const float* p, float* c, int pitch, int gy, const Region* gs, int n, Region e, int ns,
                float xcfl, float ycfl, int chunk, hipStream_t s, PipeGate gate = PipeGate{}) {
@@ -140,6 +148,7 @@ CME_EXPORT int cme_heat_pipe_gated_f32(const float* prev, float* curr, int pitch
     gate.val = value;
     gate.from = wait_from;
     gate.timeout = timeout;
+    gate.spins = gate_spin_limit();
     return fma ? pipe_order<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0, as_stream(stream),
                                   gate)
                : pipe_order<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
@@ -161,6 +170,7 @@ CME_EXPORT int cme_heat_pipe_gated_f64(const double* prev, double* curr, int pit
     gate.val = value;
     gate.from = wait_from;
     gate.timeout = timeout;
+    gate.spins = gate_spin_limit();
     return fma ? pipe_order_f64<true>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,
                                       as_stream(stream), gate)
                : pipe_order_f64<false>(order, prev, curr, pitch, gy, gs, nout, e, nsteps, xcfl, ycfl, 0,

@@ -44,12 +44,15 @@ struct PipeOut {
 // [from, n) wait until *flag >= val (wrap-safe) before reading their input
 // -- the halo exchange of the previous pass signals the flag from the comm
 // stream (dist_heat.hip). Bounded: a wait past the spin limit sets *timeout
-// (pinned host word) and proceeds. flag == nullptr: no gate.
+// (pinned host word) and proceeds. flag == nullptr: no gate. `spins`: polls
+// before giving up (~2^24: tens of seconds; CME_DIST_GATE_SPINS lowers it so
+// a test can force the timeout path).
 struct PipeGate {
     const unsigned* flag = nullptr;
     unsigned val = 0;
     int from = 0;
     unsigned* timeout = nullptr;
+    unsigned spins = 1u << 24;
 };
 
 }  // namespace cme
