@@ -164,10 +164,19 @@ def _onesweep(keys: torch.Tensor, values: torch.Tensor | None, key_bits: int):
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
-    t = _ws.get(dev.index)
+    """Scratch of the reduce-then-scan sort (tile counts and totals; every
+    call rewrites what it reads). Eager calls share one buffer per (device,
+    stream): sorts on different streams never race on it. Under stream
+    capture every call gets its own buffer from the graph's private pool, so
+    a replay never writes into memory an eager call has since replaced and
+    freed."""
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    key = (dev.index, _ext.stream_ptr(dev))
+    t = _ws.get(key)
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _ws[dev.index] = t
+        _ws[key] = t
     return t
 
 

@@ -366,6 +366,7 @@ class MatrixStats:
     ndiag: int  # occupied diagonals
     dia_fill: float  # nnz / (ndiag * nrows)
     ell_fill: float  # nnz / (max_row * nrows)
+    far_frac: float = 1.0  # nonzeros more than _CB_NEAR columns off their row's (scaled) diagonal
 
 
 def matrix_stats(a: CSR) -> MatrixStats:
@@ -379,8 +380,16 @@ def matrix_stats(a: CSR) -> MatrixStats:
     if off.size > (1 << 24):
         off = off[np.random.default_rng(0).integers(0, off.size, 1 << 22)]
     ndiag = int(np.unique(off).size)
+    # gather locality: how far a row's columns sit from its own position
+    # (scaled to the column range for rectangular matrices)
+    cols = a.col.cpu().numpy().astype(np.int64)
+    rows_s = rows * (a.ncols / max(1, a.nrows))
+    if cols.size > (1 << 24):
+        pick = np.random.default_rng(1).integers(0, cols.size, 1 << 22)
+        cols, rows_s = cols[pick], rows_s[pick]
+    far = float(np.mean(np.abs(cols - rows_s) > _CB_NEAR)) if cols.size else 0.0
     return MatrixStats(a.nrows, a.nnz, mean, mx, cv, ndiag, a.nnz / max(1, ndiag * a.nrows),
-                       a.nnz / max(1, mx * a.nrows))
+                       a.nnz / max(1, mx * a.nrows), far)
 
 
 def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
@@ -391,8 +400,9 @@ def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
       * HYB  -- ELL for the typical rows + COO for a heavy tail (power-law
                 rows would serialise CSR lanes on the longest row);
       * CSR-vector (16-B aligned rows) -- everything else, in column blocks of
-        2 MB of x when x is larger (one XCD's L2 keeps the block's x slice:
-        random 1M x 1M, 16/row: 0.0957 vs 0.1038 ms cold, profiles/spmv_cb_r3.jsonl)."""
+        2 MB of x when x is larger and most gathers land far from the
+        diagonal (one XCD's L2 keeps the block's x slice: random 1M x 1M,
+        16/row: 0.0957 vs 0.1038 ms cold, profiles/spmv_cb_r3.jsonl)."""
     st = stats or matrix_stats(a)
     if st.ndiag <= 64 and st.dia_fill >= 0.6:
         return "dia"
@@ -400,7 +410,18 @@ def choose_format(a: CSR, stats: MatrixStats | None = None) -> str:
         return "ell"
     if st.max_row > 8 * max(1.0, st.mean_row) or st.cv_row > 1.0:
         return "hyb"
-    return "csr_cb" if 4 * a.ncols > (2 << 20) else "csr_aligned"
+    # column blocks pay only when x outgrows one L2 slice AND the gathers
+    # actually roam over it; banded / reordered matrices (most nonzeros near
+    # the diagonal) keep their x reuse in one pass of the aligned CSR, which
+    # re-reads rp and y once instead of once per block
+    if 4 * a.ncols > (2 << 20) and st.far_frac > 0.5:
+        return "csr_cb"
+    return "csr_aligned"
+
+
+# |col - row| beyond this (in columns: 256 KB of fp32 x, an eighth of a
+# column block) counts as a far gather
+_CB_NEAR = 1 << 16
 
 
 def prepare(a: CSR, fmt: str = "auto", device=None):

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Overlap of two kernel families in a rocprofv3 --kernel-trace CSV.
+"""Overlap of two kernel families in a rocprofv3 --kernel-trace output (CSV
+or the default rocpd SQLite database).
 
     python scripts/overlap.py <dir with *kernel_trace.csv> --a heat_pipe --b nccl [--skip-a N]
 
@@ -29,6 +30,10 @@ def main():
     for p in glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    for p in glob.glob(os.path.join(args.dir, "**", "*.db"), recursive=True):  # rocprofv3's default rocpd output
+        import sqlite3
+
+        rows += [(int(s), int(e), n) for s, e, n in sqlite3.connect(p).execute("select start, end, name from kernels")]
     rows.sort()
     A = [r for r in rows if args.a in r[2]][args.skip_a:]
     B = [r for r in rows if args.b.lower() in r[2].lower()]

@@ -164,3 +164,38 @@ def test_hip_graph_capture_heat_stepn(gpu, kernel):
         ops.heat_step(a, b, reg, 8, xc, yc, "fma")
     torch.cuda.synchronize(gpu)
     assert torch.equal(got, ref.buf[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_values", [False, True])
+def test_hip_graph_capture_sort_then_larger_eager_sort(gpu, with_values):
+    """sort / sort_by_key captured into a HIP graph, then a LARGER
+    eager sort on the same stream (which used to replace and free the shared
+    workspace the graph still pointed at), then two replays: both equal
+    torch.sort of the captured input, and the eager sort is right too."""
+    gen = torch.Generator(device=gpu).manual_seed(11)
+    keys = torch.randint(0, 1 << 30, (300_000,), device=gpu, dtype=torch.int32, generator=gen)
+    vals = torch.arange(keys.numel(), device=gpu, dtype=torch.int32)
+
+    def f():
+        return ops.sort_by_key(keys, vals) if with_values else (ops.sort(keys), None)
+
+    s = torch.cuda.Stream(gpu)
+    s.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(s):
+        f()  # warm-up outside capture
+    torch.cuda.current_stream(gpu).wait_stream(s)
+    torch.cuda.synchronize(gpu)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        k_out, v_out = f()
+    big = torch.randint(0, 1 << 30, (5_000_000,), device=gpu, dtype=torch.int32, generator=gen)
+    big_sorted = ops.sort(big)  # eager, larger: grows the eager workspace
+    want_k, want_i = torch.sort(keys, stable=True)
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize(gpu)
+        assert torch.equal(k_out, want_k)
+        if with_values:
+            assert torch.equal(v_out, want_i.to(torch.int32))
+    assert torch.equal(big_sorted, torch.sort(big).values)

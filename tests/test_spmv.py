@@ -99,3 +99,25 @@ def test_colblocked_format_choice_and_blocks():
     want = sorted(zip(rows.tolist(), big.col.tolist(), big.val.tolist()))
     assert got == want
     assert choose_format(laplacian("5pt", 1100)) == "dia"
+
+
+def test_colblocked_needs_far_gathers():
+    """A large banded matrix that is not DIA-eligible (a random band of +-2000
+    columns around the diagonal, 4-20 per row) keeps the single-pass aligned
+    CSR: its gathers already stay local, so column blocks would only re-read
+    rp and y per block."""
+    from cme213x.ops.spmv import CSR, choose_format, matrix_stats
+
+    n = 1 << 20
+    rng = np.random.default_rng(6)
+    lens = rng.integers(4, 21, n)  # irregular rows (not ELL): 4..20, mean 12
+    rows = np.repeat(np.arange(n), lens)
+    cols = np.clip(rows + rng.integers(-2000, 2001, rows.size), 0, n - 1)
+    order = np.lexsort((cols, rows))
+    rp = np.concatenate([[0], np.cumsum(lens)])
+    a = CSR(n, n, torch.from_numpy(rp.astype(np.int32)), torch.from_numpy(cols[order].astype(np.int32)),
+            torch.ones(rows.size))
+    st = matrix_stats(a)
+    assert st.far_frac < 0.01 and st.ndiag > 64
+    assert choose_format(a, st) == "csr_aligned"
+    assert matrix_stats(random_csr(2000, 1 << 20, 12, seed=5)).far_frac > 0.8
