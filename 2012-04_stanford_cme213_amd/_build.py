@@ -32,6 +32,10 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", shutil.which("g++") or "g++")
 
 HIP_LIB = LIB_DIR / "libcme213_hip.so"
+# tuning arms (csrc/hip_tune/: the wave-pipelined pass's A/B instantiations):
+# only with CME_TUNE=1 / `make TUNE=1`, into their own library, so the
+# production library carries only what the ops dispatch to
+TUNE_LIB = LIB_DIR / "libcme213_tune.so"
 CPU_LIB = LIB_DIR / "libcme213_cpu.so"
 
 
@@ -73,13 +77,13 @@ def _newest_header() -> float:
 
 
 def _local_includes(src: Path) -> list[Path]:
-    """Headers next to a source that it #includes by quoted name (heat_pipe.h
-    is shared by heat_pipe.hip and heat_pipe_tune.hip)."""
+    """Headers a source #includes by quoted relative path (heat_pipe.h is
+    shared by heat_pipe.hip and hip_tune/heat_pipe_tune.hip)."""
     out = []
     for line in src.read_text(errors="replace").splitlines():
         line = line.strip()
-        if line.startswith('#include "') and "/" not in line:
-            h = src.parent / line.split('"')[1]
+        if line.startswith('#include "') and not line.startswith('#include "cme213/'):
+            h = (src.parent / line.split('"')[1]).resolve()
             if h.exists():
                 out.append(h)
     return out
@@ -109,7 +113,7 @@ def _compile_all(srcs: list[Path], kind: str, jobs: int, verbose: bool) -> list[
         o = out_dir / (s.stem + ".o")
         objs.append(o)
         if _needs(o, s, hdr):
-            if kind == "hip":
+            if kind in ("hip", "hip_tune"):
                 cmd = [HIPCC, *_hip_flags(), "-c", str(s), "-o", str(o)]
             else:
                 cmd = [CXX, *_cpu_flags(), "-c", str(s), "-o", str(o)]
@@ -133,16 +137,28 @@ def _link(objs: list[Path], out: Path, kind: str) -> None:
         rocm_lib = os.environ.get("ROCM_PATH", "/opt/rocm") + "/lib"
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
                f"-L{rocm_lib}", "-lrccl"]
+    elif kind == "hip_tune":
+        # resolves the runtime's symbols (kernel registry, tuning table)
+        # against libcme213_hip.so, which _ext loads first (RTLD_GLOBAL)
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     else:
         cmd = [CXX, "-shared", "-fPIC", "-fopenmp", "-o", str(tmp), *map(str, objs)]
     _run(cmd)
     os.replace(tmp, out)
 
 
-def build(jobs: int | None = None, verbose: bool = True, hip: bool = True, cpu: bool = True) -> dict:
-    """Compile every native source; returns {'hip': path|None, 'cpu': path|None}."""
+def tune_enabled() -> bool:
+    return os.environ.get("CME_TUNE", "0") not in ("", "0")
+
+
+def build(jobs: int | None = None, verbose: bool = True, hip: bool = True, cpu: bool = True,
+          tune: bool | None = None) -> dict:
+    """Compile every native source; returns {'hip': path|None, 'cpu': path|None,
+    'tune': path|None}. ``tune`` (default: CME_TUNE=1) also builds the tuning
+    arms into libcme213_tune.so."""
     jobs = jobs or min(16, os.cpu_count() or 4)
-    out: dict = {"hip": None, "cpu": None}
+    out: dict = {"hip": None, "cpu": None, "tune": None}
+    tune = tune_enabled() if tune is None else tune
     if cpu:
         srcs = sorted((CSRC / "cpu").glob("*.cpp"))
         objs = _compile_all(srcs, "cpu", jobs, verbose)
@@ -153,6 +169,11 @@ def build(jobs: int | None = None, verbose: bool = True, hip: bool = True, cpu: 
         objs = _compile_all(srcs, "hip", jobs, verbose)
         _link(objs, HIP_LIB, "hip")
         out["hip"] = HIP_LIB
+    if hip and tune:
+        srcs = sorted((CSRC / "hip_tune").glob("*.hip"))
+        objs = _compile_all(srcs, "hip_tune", jobs, verbose)
+        _link(objs, TUNE_LIB, "hip_tune")
+        out["tune"] = TUNE_LIB
     return out
 
 

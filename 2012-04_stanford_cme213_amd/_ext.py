@@ -39,6 +39,9 @@ _CT = {
 # name -> argument signature (return type is always int)
 HIP_PROTOS: dict[str, str] = {"cme_device_sync": ""}
 CPU_PROTOS: dict[str, str] = {}
+# entry points of the tuning library (libcme213_tune.so, built with CME_TUNE=1 /
+# `make TUNE=1`); call_hip routes these names there
+TUNE_PROTOS: dict[str, str] = {}
 
 
 def proto(table: dict, name: str, sig: str) -> None:
@@ -53,8 +56,10 @@ def _fn(kind: str, name: str):
     key = (kind, name)
     f = _bound.get(key)
     if f is None:
+        if kind == "hip" and name in TUNE_PROTOS:
+            kind = "tune"
         lib = _load(kind)
-        protos = HIP_PROTOS if kind == "hip" else CPU_PROTOS
+        protos = {"hip": HIP_PROTOS, "tune": TUNE_PROTOS}.get(kind, CPU_PROTOS)
         if name not in protos:
             raise KeyError(f"no prototype registered for {kind}:{name}")
         f = getattr(lib, name)
@@ -66,29 +71,37 @@ def _fn(kind: str, name: str):
 
 def _load(kind: str) -> ctypes.CDLL:
     with _lock:
-        if kind in _libs:
-            return _libs[kind]
-        path = _LIB_DIR / f"libcme213_{kind}.so"
-        alt = os.environ.get(f"CME_{kind.upper()}_LIB")  # experiments: an alternative build of the library
-        if alt:
-            path = Path(alt)
-        if not path.exists():
-            if os.environ.get("CME_AUTOBUILD", "1") != "0":
-                from . import _build
+        return _load_unlocked(kind)
 
-                _build.build(hip=(kind == "hip"), cpu=(kind == "cpu"), verbose=True)
-            if not path.exists():
-                raise RuntimeError(f"cme213x native library missing: {path} (run __graft_entry__.build())")
-        # torch is imported first so its bundled libamdhip64.so.7 (same SONAME)
-        # is the one our HIP library binds to: one HIP runtime per process.
-        lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
-        if kind == "hip":
-            lib.cme_hip_error_string.restype = ctypes.c_char_p
-            lib.cme_hip_error_string.argtypes = [ctypes.c_int]
-            lib.cme_rccl_error_string.restype = ctypes.c_char_p
-            lib.cme_rccl_error_string.argtypes = [ctypes.c_int]
-        _libs[kind] = lib
-        return lib
+
+def _load_unlocked(kind: str) -> ctypes.CDLL:
+    if kind in _libs:
+        return _libs[kind]
+    if kind == "tune":
+        # its undefined runtime symbols resolve against the HIP library
+        _libs.get("hip") or _load_unlocked("hip")
+    path = _LIB_DIR / f"libcme213_{kind}.so"
+    alt = os.environ.get(f"CME_{kind.upper()}_LIB")  # experiments: an alternative build of the library
+    if alt:
+        path = Path(alt)
+    if not path.exists():
+        if os.environ.get("CME_AUTOBUILD", "1") != "0":
+            from . import _build
+
+            _build.build(hip=(kind in ("hip", "tune")), cpu=(kind == "cpu"), verbose=True,
+                         tune=True if kind == "tune" else None)
+        if not path.exists():
+            raise RuntimeError(f"cme213x native library missing: {path} (run __graft_entry__.build())")
+    # torch is imported first so its bundled libamdhip64.so.7 (same SONAME)
+    # is the one our HIP library binds to: one HIP runtime per process.
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    if kind == "hip":
+        lib.cme_hip_error_string.restype = ctypes.c_char_p
+        lib.cme_hip_error_string.argtypes = [ctypes.c_int]
+        lib.cme_rccl_error_string.restype = ctypes.c_char_p
+        lib.cme_rccl_error_string.argtypes = [ctypes.c_int]
+    _libs[kind] = lib
+    return lib
 
 
 def hip() -> ctypes.CDLL:

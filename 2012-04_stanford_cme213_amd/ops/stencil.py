@@ -23,9 +23,11 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step2_f64", "ppiipipiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f32", "ppiipipiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_stepn_f64", "ppiipipiiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f32", "ppiipipiiffiip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_f32", "ppiiiiiiiiffip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f64", "ppiipipiiddiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_gate_status", "p")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_gated_f32", "ppiipipiiffiipupp")
@@ -43,19 +45,24 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_fast_f64", "ppiiiiiidd")
 VARIANTS = {"naive": 0, "global": 0, "lds": 1, "shared": 1, "stream": 2, "lds_nopad": 3, "stream2": 4,
             "stream2_fma": 5, "stream_fma": 6, "fma": 6, "stream3": 7, "stream3_fma": 8, "stream4": 9,
             "stream4_fma": 10, "pipe3": 11, "pipe3_fma": 12, "pipe4": 13, "pipe4_fma": 14, "pipe5": 15,
-            "pipe5_fma": 16, "pipe6": 17, "pipe6_fma": 18}
+            "pipe5_fma": 16, "pipe6": 17, "pipe6_fma": 18, "tile1": 19, "tile1_fma": 20, "tile2": 21,
+            "tile2_fma": 22, "tile3": 23, "tile3_fma": 24, "tile4": 25, "tile4_fma": 26}
 # variants that advance more than one timestep per launch (multi-step drivers
 # only); stream4 (4 steps per HBM pass) is fp32 only, stream3 takes fp32 and
 # fp64 (one row per register block for doubles); pipeN = the wave-pipelined
 # N-step pass (csrc/hip/heat_pipe.hip), fp32 and fp64 (pipe5 / pipe6: fp32, for
 # the HBM-bound low orders)
 MULTISTEP = {"stream2", "stream2_fma", "stream3", "stream3_fma", "stream4", "stream4_fma", "pipe3", "pipe3_fma",
-             "pipe4", "pipe4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma"}
+             "pipe4", "pipe4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma", "tile2", "tile2_fma", "tile3",
+             "tile3_fma", "tile4", "tile4_fma"}
+# tileN[_fma]: N steps per pass of the LDS-resident tile kernel (csrc/hip/heat_tile.hip) -- small grids
+# (the hw5 shapes), whole-interior runs only (heat_run)
+TILE_VARIANTS = {"tile1", "tile1_fma", "tile2", "tile2_fma", "tile3", "tile3_fma", "tile4", "tile4_fma"}
 FP32_ONLY = {"stream4", "stream4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma"}
 # FMA-contracted stencil (heat_update_fma); on CPU tensors these select the
 # std::fma oracle, every other variant name the exact (contraction-off) one
 FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma",
-                "pipe5_fma", "pipe6_fma"}
+                "pipe5_fma", "pipe6_fma", "tile1_fma", "tile2_fma", "tile3_fma", "tile4_fma"}
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -75,8 +82,8 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
               xcfl: float, ycfl: float, variant: str = "stream", chunk: int = 0) -> None:
     """curr[region] = FTCS(prev); region = (xb, xe, yb, ye) in grid coords."""
     _check(prev, curr)
-    if variant in MULTISTEP:
-        raise ValueError(f"variant {variant!r} advances two steps per launch; use heat_run")
+    if variant in MULTISTEP or variant in TILE_VARIANTS:
+        raise ValueError(f"variant {variant!r} is a multi-step / whole-interior pass; use heat_run")
     xb, xe, yb, ye = map(int, region)
     rows, pitch = prev.shape
     f64 = prev.dtype == torch.float64
@@ -160,6 +167,22 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
         name = "cme_heat_pipe_f64" if f64 else "cme_heat_pipe_f32"
     _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r), len(regions),
                   ctypes.addressof(e), order, nsteps, xcfl, ycfl, chunk, int(fma), _ext.stream_ptr(prev.device))
+
+
+def heat_tile(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
+              ycfl: float, nsteps: int, fma: bool = False) -> None:
+    """ONE ``nsteps``-step (1-4) pass of the LDS-resident tile kernel
+    (``csrc/hip/heat_tile.hip``): curr[region] = FTCS^nsteps(prev). Every
+    cell outside ``region`` must hold the same fixed value in both buffers
+    (the Dirichlet ghost layer of a whole-interior run)."""
+    _check(prev, curr)
+    if not prev.is_cuda:
+        raise ValueError("heat_tile: GPU only")
+    xb, xe, yb, ye = map(int, region)
+    rows, pitch = prev.shape
+    name = "cme_heat_tile_f64" if prev.dtype == torch.float64 else "cme_heat_tile_f32"
+    _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, xb, xe, yb, ye, order, int(nsteps), xcfl,
+                  ycfl, int(fma), _ext.stream_ptr(prev.device))
 
 
 def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,

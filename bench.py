@@ -279,6 +279,9 @@ def main() -> int:
         schedule = "python passes" if comm.size > 1 else "heat_run (one native call)"
     pts = args.n * args.n
     bpp = bytes_per_point(args.order, torch.float32)
+    from cme213x.utils import tuning
+
+    pipe_vw = tuning.get("pipe_vw") if on_gpu else 0
     eff = pts * bpp * args.steps / secs / 1e9
     # min HBM traffic: one read + one write of the grid per PASS (a pass
     # advances `tblock` timesteps)
@@ -307,8 +310,8 @@ def main() -> int:
                             f"{'pipe' if args.kernel == 'pipe' and args.tblock >= 3 else 'stream'}{args.tblock} "
                             f"({args.tblock} steps/pass)") + (" fma" if args.fma else " exact"),
                 "kernel": args.kernel,
-                # pipelined fp32 pass: 8 columns per lane at order 8 (CME_PIPE_VW=4 / 8 forces one width)
-                "lane_columns": ({"4": 4, "8": 8}.get(os.environ.get("CME_PIPE_VW", ""), 8 if args.order == 8 else 4)
+                # pipelined fp32 pass: 8 columns per lane at order 8 (tuning knob pipe_vw = 4 / 8 forces one width)
+                "lane_columns": ({4: 4, 8: 8}.get(pipe_vw, 8 if args.order == 8 else 4)
                                  if args.kernel == "pipe" and args.tblock >= 3 else 4),
                 "fma": bool(args.fma),
                 "tblock": args.tblock,

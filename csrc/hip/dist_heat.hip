@@ -37,6 +37,7 @@
 #include <string>
 
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/heat_region.h"
 
 extern "C" int cme_heat_step_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
@@ -616,11 +617,9 @@ int get_ctx(int nsub, DistCtx** out) {
         // dist_rank_r2.md) the default system-scope record is no slower
         // (0.0321-0.0322 vs 0.0334-0.0338 ms/step), so it stays the default.
         // CME_DIST_EVENT_SCOPE=device selects hipEventReleaseToDevice.
-        static const unsigned evf = [] {
-            const char* e = getenv("CME_DIST_EVENT_SCOPE");
-            return (e && strcmp(e, "device") == 0) ? (unsigned)(hipEventDisableTiming | hipEventReleaseToDevice)
-                                                   : (unsigned)hipEventDisableTiming;
-        }();
+        const unsigned evf = cme::tune_get(cme::kTuneDistEventScope) == 1
+                                 ? (unsigned)(hipEventDisableTiming | hipEventReleaseToDevice)
+                                 : (unsigned)hipEventDisableTiming;
         for (int k = 0; k < 2; ++k) {
             CME_TRY(hipEventCreateWithFlags(&u.ev_border[k], evf));
             CME_TRY(hipEventCreateWithFlags(&u.ev_int[k], evf));
@@ -821,7 +820,7 @@ int local_peers(const SubDesc* subs, int nsub, int si, int* out) {
 // never under stream capture). Returns 0 and sets u.probe.
 int run_gate_probe(SubCtx& u) {
     if (u.probe != 0) return 0;
-    static const bool verbose = getenv("CME_DIST_VERBOSE") != nullptr;
+    const bool verbose = cme::tune_get(cme::kTuneDistVerbose) != 0;
     *u.probe_result = 0u;
     CME_TRY(hipMemsetAsync(u.probe_word, 0, sizeof(unsigned), u.compute));
     CME_TRY(hipStreamSynchronize(u.compute));
@@ -873,10 +872,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     // || interior stream; 1: border then interior on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for
     // re-measuring on other topologies.
-    static const int schedule = [] {
-        const char* e = getenv("CME_DIST_SCHEDULE");
-        return e ? atoi(e) : 2;
-    }();
+    const int schedule = (int)cme::tune_get(cme::kTuneDistSchedule);
     // 2 (fused): ONE pipelined launch per pass holding the deep interior and
     // the border strips; the border workgroups (last in the grid) wait
     // in-kernel for the previous exchange's flag, so the compute queue never
@@ -909,10 +905,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     // benchmarks/bench_dist_rank.py); the other transports hold their comm
     // stream that long before each exchange (a test forces the fused gate's
     // timeout path this way)
-    const int fake_us = [] {
-        const char* e = getenv("CME_DIST_FAKE_XCHG_US");
-        return e ? atoi(e) : 0;
-    }();
+    const int fake_us = (int)cme::tune_get(cme::kTuneDistFakeXchgUs);
     // Exchange the halos of state k for every sub. The caller has made each
     // comm stream wait for what the exchange reads; ev_comm is recorded after.
     auto exchange_all = [&](int k) -> int {

@@ -22,6 +22,7 @@
 //            next RB rows are prefetched while the current RB are computed.
 //            Each input element is fetched from HBM ~once: 8 B/pt fp32.
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/heat_region.h"
 #include "cme213/heat_stencil.h"
 #include "cme213/vec.h"
@@ -594,10 +595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // the row chunk (more, shorter chunks win for the lighter FMA kernel).
 template <typename T, bool FMA, int RB>
 int stream2_chunk(int strips, int H, int chunk_hint) {
-    static const int env_chunk = [] {
-        const char* e = getenv("CME_STREAM2_CHUNK");  // tuning experiments only
-        return e ? atoi(e) : 0;
-    }();
+    const int env_chunk = (int)cme::tune_get(cme::kTuneStream2Chunk);  // tuning experiments only
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
         const long target_waves = 256L * (sizeof(T) == 4 ? (FMA ? 128 : 48) : 24);
@@ -662,26 +660,13 @@ int launch_stream2_multi(const T* prev, T* curr, int pitch, int gy, const Region
 // about 1024 waves.
 template <int NS, int RB>
 int streamn_chunk(int strips, int H, int chunk_hint, long cap) {
-    static const int env_chunk = [] {
-        const char* e = getenv("CME_STREAMN_CHUNK");
-        return e ? atoi(e) : 0;
-    }();
-    static const int env_rounds = [] {
-        const char* e = getenv("CME_STREAMN_ROUNDS");
-        return e ? atoi(e) : 0;
-    }();
-    static const int env_min = [] {
-        const char* e = getenv("CME_STREAMN_MINCHUNK");
-        return e ? atoi(e) : 0;
-    }();
-    static const long thin_waves = [] {
-        const char* e = getenv("CME_STREAMN_THIN_WAVES");
-        return e && atoi(e) > 0 ? (long)atoi(e) : 1024L;
-    }();
-    static const int cap_pct = [] {  // share of the resident waves a bulk region may take
-        const char* e = getenv("CME_STREAMN_CAPPCT");
-        return e && atoi(e) > 0 ? atoi(e) : 100;
-    }();
+    const int env_chunk = (int)cme::tune_get(cme::kTuneStreamNChunk);
+    const int env_rounds = (int)cme::tune_get(cme::kTuneStreamNRounds);
+    const int env_min = (int)cme::tune_get(cme::kTuneStreamNMinChunk);
+    const long thin_waves = cme::tune_get(cme::kTuneStreamNThinWaves) > 0 ? cme::tune_get(cme::kTuneStreamNThinWaves)
+                                                                          : 1024L;
+    // share of the resident waves a bulk region may take
+    const int cap_pct = cme::tune_get(cme::kTuneStreamNCapPct) > 0 ? (int)cme::tune_get(cme::kTuneStreamNCapPct) : 100;
     cap = cap * cap_pct / 100;
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
@@ -997,11 +982,29 @@ CME_EXPORT int cme_heat_step_f64(const double* prev, double* curr, int pitch, in
                                  as_stream(stream));
 }
 
+extern "C" int cme_heat_tile_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
+                                 int order, int nsteps, float xcfl, float ycfl, int fma, void* stream);
+extern "C" int cme_heat_tile_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb,
+                                 int ye, int order, int nsteps, double xcfl, double ycfl, int fma, void* stream);
+
+namespace {
+int tile_pass_t(const float* p, float* c, int pitch, int gy, Region g, int order, int ns, int fma, float xc,
+                float yc, hipStream_t s) {
+    return cme_heat_tile_f32(p, c, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, ns, xc, yc, fma, (void*)s);
+}
+int tile_pass_t(const double* p, double* c, int pitch, int gy, Region g, int order, int ns, int fma, double xc,
+                double yc, hipStream_t s) {
+    return cme_heat_tile_f64(p, c, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, ns, xc, yc, fma, (void*)s);
+}
+}  // namespace
+
 // Multi-step driver: `iters` sweeps of the full region in one call (buffers
 // a/b, first sweep reads a). Avoids per-iteration host round trips (the
 // reference synchronises after every launch: 2dHeat_solution.cu:549).
 // variants 4/5 advance TWO steps per launch (+ one single step, variant 2/6,
-// for odd iters).
+// for odd iters). Variants 19..26: tileN exact / FMA, N = 1..4 steps per
+// pass of the LDS-resident tile kernel (heat_tile.hip, small grids), the
+// remainder as one shorter tile pass.
 // *final_idx = 0 if the result is in a, 1 if in b.
 template <typename T>
 int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int variant, T xcfl, T ycfl, int iters,
@@ -1009,6 +1012,18 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int cur = 0;
     T* bufs[2] = {a, b};
     int i = 0;
+    if (variant >= 19 && variant <= 26) {
+        const int ns = (variant - 19) / 2 + 1, fma = (variant - 19) & 1;
+        while (i < iters) {
+            const int k = iters - i < ns ? iters - i : ns;
+            int rc = tile_pass_t(bufs[cur], bufs[cur ^ 1], pitch, gy, g, order, k, fma, xcfl, ycfl, s);
+            if (rc) return rc;
+            cur ^= 1;
+            i += k;
+        }
+        *final_idx = cur;
+        return 0;
+    }
     if (variant >= 7 && variant <= 18) {
         if (sizeof(T) != 4 && (variant == 9 || variant == 10 || variant >= 15)) return (int)hipErrorInvalidValue;
         const int ns = variant >= 11 ? (variant - 11) / 2 + 3 : (variant <= 8 ? 3 : 4);

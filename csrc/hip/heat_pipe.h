@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/heat_region.h"
 #include "cme213/heat_stencil.h"
 #include "cme213/vec.h"
@@ -462,18 +463,9 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
 // for sweeps (per_cu = task target per CU).
 template <int NS, int RB, int VW = 4>
 int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident, bool thin_floor) {
-    static const int env_chunk = [] {
-        const char* e = getenv("CME_PIPE_CHUNK");
-        return e ? atoi(e) : 0;
-    }();
-    static const int env_per_cu = [] {
-        const char* e = getenv("CME_PIPE_PER_CU");
-        return e ? atoi(e) : 0;
-    }();
-    static const int thin_min = [] {
-        const char* e = getenv("CME_PIPE_THIN_MIN");
-        return e ? atoi(e) : 64;
-    }();
+    const int env_chunk = (int)cme::tune_get(cme::kTunePipeChunk);
+    const int env_per_cu = (int)cme::tune_get(cme::kTunePipePerCU);
+    const int thin_min = (int)cme::tune_get(cme::kTunePipeThinMin);
     int chunk = chunk_hint > 0 ? chunk_hint : env_chunk;
     if (chunk <= 0) {
         const int per_cu = per_cu_hint > 0 ? per_cu_hint : env_per_cu;

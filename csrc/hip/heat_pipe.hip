@@ -14,12 +14,8 @@ namespace {
 // CME_PIPE_VW: unset = the measured default (8 columns per lane at order 8,
 // 4 at orders 2 / 4), 4 / 8 = that width at every order
 int pipe_vw_env() {
-    static const int v = [] {
-        const char* e = getenv("CME_PIPE_VW");
-        const int x = e ? atoi(e) : 0;
-        return (x == 4 || x == 8) ? x : 0;
-    }();
-    return v;
+    const long x = cme::tune_get(cme::kTunePipeVW);
+    return (x == 4 || x == 8) ? (int)x : 0;
 }
 
 template <int ORDER, bool FMA>
@@ -48,8 +44,7 @@ int pipe_ns(const float* p, float* c, int pitch, int gy, const Region* gs, int n
 // poll bound of the fused schedule's gated border workgroups (PipeGate):
 // CME_DIST_GATE_SPINS, read per call (a test forces the timeout path in-process)
 unsigned gate_spin_limit() {
-    const char* e = getenv("CME_DIST_GATE_SPINS");
-    const long v = e ? atol(e) : 0;
+    const long v = cme::tune_get(cme::kTuneDistGateSpins);
     return v > 0 ? (unsigned)v : (1u << 24);
 }
 

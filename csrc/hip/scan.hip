@@ -15,6 +15,7 @@
 //  * cme_spmv_scan_step fused final-project step: a[i] *= xx[i] then inclusive
 //                       segmented scan of a (segment heads as a bitmask).
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/lookback.h"
 #include "cme213/wave.h"
 
@@ -1136,10 +1137,7 @@ CME_EXPORT int cme_spmv_scan_run(float* a, const float* xx, const uint32_t* flag
                                  void* stream) {
     if (n <= 0 || iters <= 0) return 0;
     const long long tiles = (n + 4095) / 4096;
-    static const bool multi = [] {  // CME_SPMVSCAN_MULTI=0: one launch per step (the round-2 path)
-        const char* e = getenv("CME_SPMVSCAN_MULTI");
-        return !(e && atoi(e) == 0);
-    }();
+    const bool multi = cme::tune_get(cme::kTuneSpmvScanMulti) != 0;  // 0: one launch per step (the round-2 path)
     static int bpc = persistent_blocks_per_cu(segscan_kernel<1, true, 4, true, true>, kScanThreads);
     hipStream_t s = as_stream(stream);
     if (multi) {

@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/wave.h"
 
 using namespace cme;
@@ -534,12 +535,8 @@ __global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_
 // 0.363 / 0.391 ms at caps 1024 / 2048 / 4096 (48M: 1.18 / 1.13 / 1.14).
 // CME_RADIX_MAXBLOCKS overrides the cap (<= kMaxRadixBlocks, sweeps).
 static int radix_max_blocks() {
-    static const int v = [] {
-        const char* e = getenv("CME_RADIX_MAXBLOCKS");
-        int x = e ? atoi(e) : 1024;
-        return x < 1 ? 1 : (x > kMaxRadixBlocks ? kMaxRadixBlocks : x);
-    }();
-    return v;
+    const long x = cme::tune_get(cme::kTuneRadixMaxBlocks);
+    return x < 1 ? 1 : (x > kMaxRadixBlocks ? kMaxRadixBlocks : (int)x);
 }
 
 CME_EXPORT long long cme_radix_ws_bytes(long long n) {
@@ -557,13 +554,7 @@ CME_EXPORT long long cme_radix_ws_bytes(long long n) {
 // (0.348-0.357 ms; the ranking's LDS round trips are not what binds), the
 // prefetch without atomic ranks is best at 48M (0.956 vs 0.981 ms;
 // profiles/sort_r3.md)
-static int radix_ds_variant() {
-    static const int v = [] {
-        const char* e = getenv("CME_RADIX_DS");
-        return e ? (atoi(e) & 7) : 2;
-    }();
-    return v;
-}
+static int radix_ds_variant() { return (int)(cme::tune_get(cme::kTuneRadixDS) & 7); }
 
 CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
                               uint32_t* vtmp, long long n, int mode, int bit0, int bit1, void* ws, void* stream) {

@@ -20,6 +20,7 @@
 //               takes 4 consecutive nonzeros with one 16-B value load and one
 //               16-B index load
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/wave.h"
 
 using namespace cme;
@@ -308,10 +309,7 @@ CME_EXPORT int cme_spmv_csr_aligned(int nrows, const int* rp, const int* col, co
     hipStream_t s = as_stream(stream);
     if (((uintptr_t)col % 16) || ((uintptr_t)val % 16)) return (int)hipErrorInvalidValue;
     // CME_SPMV_NT=0/1 selects the stream loads (default: non-temporal)
-    static const bool nt = [] {
-        const char* e = getenv("CME_SPMV_NT");
-        return e ? atoi(e) != 0 : true;
-    }();
+    const bool nt = cme::tune_get(cme::kTuneSpmvNT) != 0;
     switch (group) {
 #define V(G)                                                                                                      \
     case G:                                                                                                       \
@@ -342,7 +340,7 @@ CME_EXPORT int cme_spmv_dia(int nrows, int ncols, int ndiag, const int* offsets,
     // SIMD): with 1M rows its 250K lanes lose to the one-row kernel (27-point
     // Laplacian 41 vs 30 us, 5-point 11.0 vs 10.2 us; 16M-row 5-point 99 vs
     // 117 us -- profiles/spmv_r2.md). CME_SPMV_DIA1 forces the one-row kernel.
-    static const bool one_row = getenv("CME_SPMV_DIA1") != nullptr;
+    const bool one_row = cme::tune_get(cme::kTuneSpmvDia1) != 0;
     if (nrows % 4 == 0 && nrows >= (4 << 20) && !one_row) {
         hipLaunchKernelGGL(dia4_kernel, dim3(cdiv(nrows / 4, 256)), dim3(256), 0, as_stream(stream), nrows, ncols,
                            ndiag, offsets, data, x, y, beta);

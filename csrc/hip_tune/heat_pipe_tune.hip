@@ -1,6 +1,6 @@
 // Tuning arms of the wave-pipelined heat pass (kernel: heat_pipe.h):
 // rows per phase, prefetch depth, steps per pass, waves per role, wide lanes.
-#include "heat_pipe.h"
+#include "../hip/heat_pipe.h"
 
 // Tuning entry for the wave-pipelined NS-step pass (order 8, FMA): ns 3..6,
 // rows per phase rb, input prefetch depth pd, explicit chunk or tasks per CU.

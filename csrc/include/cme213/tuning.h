@@ -1,0 +1,41 @@
+// Process-wide tuning knobs of the native library (arm selection, chunk
+// heights, spin bounds, rehearsal delays) -- ONE table, read per call.
+//
+// Every knob starts from its CME_* environment variable (or the measured
+// default) the first time it is read, and can be changed at run time through
+// cme_tune_set / cme_tune_reset (Python: cme213x.utils.tuning), so a test or
+// a sweep selects an arm in-process instead of spawning a subprocess with a
+// different environment. Launchers read the knob on every call (one relaxed
+// atomic load); nothing caches it in a function-local static.
+#pragma once
+
+namespace cme {
+
+enum TuneKey : int {
+    kTunePipeVW = 0,       // CME_PIPE_VW: 0 measured default (8 columns per lane at order 8), 4 / 8 forced
+    kTunePipeChunk,        // CME_PIPE_CHUNK: rows per pipelined-pass task (0 = rule)
+    kTunePipePerCU,        // CME_PIPE_PER_CU: task target per CU (0 = rule)
+    kTunePipeThinMin,      // CME_PIPE_THIN_MIN: minimum chunk of thin (border) regions
+    kTuneDistSchedule,     // CME_DIST_SCHEDULE: 2 fused (default), 0 events, 1 one stream
+    kTuneDistEventScope,   // CME_DIST_EVENT_SCOPE: 0 system-scope events, 1 device-scope
+    kTuneDistVerbose,      // CME_DIST_VERBOSE: log the queue probe
+    kTuneDistGateSpins,    // CME_DIST_GATE_SPINS: polls of a fused border wait before it gives up
+    kTuneDistFakeXchgUs,   // CME_DIST_FAKE_XCHG_US: rehearsal / test delay of each exchange
+    kTuneRadixMaxBlocks,   // CME_RADIX_MAXBLOCKS: reduce-then-scan grid cap
+    kTuneRadixDS,          // CME_RADIX_DS: downsweep arm bits (1 atomic ranks, 2 prefetch, 4 8192-key tiles)
+    kTuneStream2Chunk,     // CME_STREAM2_CHUNK
+    kTuneStreamNChunk,     // CME_STREAMN_CHUNK
+    kTuneStreamNRounds,    // CME_STREAMN_ROUNDS
+    kTuneStreamNMinChunk,  // CME_STREAMN_MINCHUNK
+    kTuneStreamNThinWaves, // CME_STREAMN_THIN_WAVES
+    kTuneStreamNCapPct,    // CME_STREAMN_CAPPCT
+    kTuneSpmvScanMulti,    // CME_SPMVSCAN_MULTI
+    kTuneSpmvNT,           // CME_SPMV_NT
+    kTuneSpmvDia1,         // CME_SPMV_DIA1
+    kTuneCount
+};
+
+// Current value of a knob (its environment variable or default until set).
+long tune_get(TuneKey k);
+
+}  // namespace cme

@@ -30,3 +30,15 @@ def gpu():
 
     cme213x._ext.hip()  # must load: fail loudly on a GPU box
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def tune_lib(gpu):
+    """The tuning-arm library (libcme213_tune.so: `make TUNE=1` / CME_TUNE=1).
+    Not part of the production build, so its arm tests skip without it."""
+    import cme213x
+
+    if not (cme213x._ext._LIB_DIR / "libcme213_tune.so").exists():
+        pytest.skip("tuning library not built (make TUNE=1)")
+    cme213x._ext._load("tune")
+    return True

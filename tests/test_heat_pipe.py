@@ -125,7 +125,7 @@ def test_gpu_pipe_multi_region_ext(gpu, ns, fma):
 
 
 @pytest.mark.gpu
-def test_gpu_pipe_tuning_arms_bitwise(gpu):
+def test_gpu_pipe_tuning_arms_bitwise(gpu, tune_lib):
     """Every compiled tuning arm (ns 3-6, rows per phase, prefetch depth,
     tasks per CU / explicit chunk) equals ns single FMA steps on an odd-sized
     region of random data."""
@@ -153,7 +153,7 @@ def test_gpu_pipe_tuning_arms_bitwise(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("region", [(9, 1400, 6, 690), (130, 131, 5, 200), (4, 484, 4, 100), (600, 1100, 33, 47)])
-def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
+def test_gpu_pipe_multiwave_roles_bitwise(gpu, tune_lib, region):
     """Two and four waves per timestep role (seam x-neighbours through the LDS
     edge buffer): equal to ns single FMA steps on regions narrower than, equal
     to and wider than one strip, with explicit short chunks and the default
@@ -182,7 +182,7 @@ def test_gpu_pipe_multiwave_roles_bitwise(gpu, region):
 @pytest.mark.gpu
 @pytest.mark.parametrize("region", [(9, 1400, 6, 690), (130, 131, 5, 200), (4, 484, 4, 100), (600, 1100, 33, 47),
                                     (4, 1504, 4, 704), (12, 20, 4, 704)])
-def test_gpu_pipe_wide_lanes_bitwise(gpu, region):
+def test_gpu_pipe_wide_lanes_bitwise(gpu, tune_lib, region):
     """Wide lanes (8 columns per lane, strips on 8-column boundaries, so edge
     lanes straddle region starts like x = 4, 9, 12): equal to ns single FMA
     steps for ns 3-5, 2 and 4 rows per phase, chain-major (81) and term-major
@@ -266,7 +266,7 @@ def test_fast_oracle_close_to_exact():
 
 
 @pytest.mark.gpu
-def test_gpu_pipe_fast_arms_bitwise(gpu):
+def test_gpu_pipe_fast_arms_bitwise(gpu, tune_lib):
     """The reassociated-arithmetic tuning arms (pd 12: default registers, 13:
     capped at 4 waves/SIMD, 91: wide lanes) equal ns steps of the CPU fast
     oracle bit for bit."""

@@ -174,27 +174,22 @@ def test_merge_sort_skewed_and_stable(gpu, kind):
 @pytest.mark.gpu
 @pytest.mark.parametrize("arm", [0, 1, 3, 4, 5, 7])
 def test_radix_downsweep_arms(gpu, arm):
-    """Every reduce-then-scan downsweep arm (CME_RADIX_DS: atomic ranks,
-    next-tile prefetch, 8192-key tiles; read once per process, so each arm
-    runs in its own process) sorts keys and key-value pairs stably."""
-    import os
-    import subprocess
-    import sys
+    """Every reduce-then-scan downsweep arm (tuning knob radix_ds: atomic
+    ranks, next-tile prefetch, 8192-key tiles) sorts keys and key-value pairs
+    stably -- selected in-process through the tuning table."""
+    from cme213x.ops.sort import sort
+    from cme213x.utils import tuning
 
-    code = (
-        "import torch, cme213x\n"
-        "from cme213x.ops.sort import sort\n"
-        "g = torch.Generator(device='cuda').manual_seed(5)\n"
-        "for n in (1, 4097, 1 << 20, 3 * (1 << 20) + 77):\n"
-        "    k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device='cuda', dtype=torch.int32, generator=g)\n"
-        "    k[: n // 3] = k[: n // 3] % 7\n"
-        "    v = torch.arange(n, device='cuda', dtype=torch.int32)\n"
-        "    ks, vs = sort(k, values=v, algo='radix')\n"
-        "    rk, ri = torch.sort(k.cpu().long(), stable=True)\n"
-        "    assert torch.equal(ks.cpu().long(), rk), n\n"
-        "    assert torch.equal(vs.cpu().long(), ri), n\n"
-        "    assert torch.equal(sort(k, algo='radix').cpu().long(), rk), n\n"
-        "print('ok')\n")
-    env = dict(os.environ, CME_RADIX_DS=str(arm))
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    with tuning.override(radix_ds=arm):
+        assert tuning.get("radix_ds") == arm
+        for n in (1, 4097, 1 << 20, 3 * (1 << 20) + 77):
+            k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+            k[: n // 3] = k[: n // 3] % 7
+            v = torch.arange(n, device="cuda", dtype=torch.int32)
+            ks, vs = sort(k, values=v, algo="radix")
+            rk, ri = torch.sort(k.cpu().long(), stable=True)
+            assert torch.equal(ks.cpu().long(), rk), n
+            assert torch.equal(vs.cpu().long(), ri), n
+            assert torch.equal(sort(k, algo="radix").cpu().long(), rk), n
+    assert not tuning.is_set("radix_ds")  # restored to the environment default

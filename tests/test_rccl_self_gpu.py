@@ -208,8 +208,8 @@ def test_run_uses_native_rccl_self_peer(gpu):
 def test_gate_timeout_raises_from_run(gpu, monkeypatch):
     """A fused border wait that gives up must raise from DistHeat.run (the
     sticky pinned word is read after the final sync), not leave a silently
-    wrong state: one poll allowed (CME_DIST_GATE_SPINS=1) against an
-    exchange held back 20 ms (CME_DIST_FAKE_XCHG_US)."""
+    wrong state: one poll allowed (tuning knob dist_gate_spins=1) against
+    an exchange held back 20 ms (dist_fake_xchg_us)."""
     from cme213x.models.heat2d_dist import DistHeat
 
     p = _params(1, iters=12)
@@ -220,12 +220,11 @@ def test_gate_timeout_raises_from_run(gpu, monkeypatch):
     assert info["loop"] == "native" and info["transport"] == "loopback" and info["fused_allowed"]
     sim.run(8)
     assert sim.native_info["schedule"] == "fused"
-    monkeypatch.setenv("CME_DIST_GATE_SPINS", "1")
-    monkeypatch.setenv("CME_DIST_FAKE_XCHG_US", "20000")
-    with pytest.raises(RuntimeError, match="timed out"):
-        sim.run(12)
-    monkeypatch.delenv("CME_DIST_GATE_SPINS")
-    monkeypatch.delenv("CME_DIST_FAKE_XCHG_US")
+    from cme213x.utils import tuning
+
+    with tuning.override(dist_gate_spins=1, dist_fake_xchg_us=20000):
+        with pytest.raises(RuntimeError, match="timed out"):
+            sim.run(12)
     sim.run(4)  # the sticky word was cleared by the check: later runs report only their own waits
 
 
@@ -238,13 +237,14 @@ def test_run_hw5_fused_selftest_failure_falls_back_to_schedule0(gpu, tmp_path, m
     now in the solver."""
     from cme213x.models.heat2d_dist import run_hw5
 
+    from cme213x.utils import tuning
+
     prm = tmp_path / "params.in"
     prm.write_text("333 270\n1 1\n1\n12\n8\n5\n1\n0\n1 10 3 7\n")
     monkeypatch.chdir(tmp_path)
-    monkeypatch.setenv("CME_DIST_GATE_SPINS", "1")
-    monkeypatch.setenv("CME_DIST_FAKE_XCHG_US", "20000")
-    res = run_hw5(str(prm), None, torch.float32, "cuda:0", write_files=False, tblock=4, fma=True, kernel="pipe",
-                  native="on", periodic=(False, True))
+    with tuning.override(dist_gate_spins=1, dist_fake_xchg_us=20000):
+        res = run_hw5(str(prm), None, torch.float32, "cuda:0", write_files=False, tblock=4, fma=True,
+                      kernel="pipe", native="on", periodic=(False, True))
     info = res["sim"].native_info
     assert info["loop"] == "native" and info["fused_allowed"] is False and info["schedule"] == "events", info
     out = capsys.readouterr().out
