@@ -405,6 +405,8 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
     const int k = wv / WPR, sub = wv % WPR;
     int task = (int)blockIdx.x;
     if (task >= R.wave_end[R.n - 1]) return;  // whole workgroup
+    unsigned long long t_start = 0;
+    if (gate.trace && threadIdx.x == 0) t_start = wall_clock64();
     int r = 0;
     while (task >= R.wave_end[r]) ++r;
     if (r > 0) task -= R.wave_end[r - 1];
@@ -452,6 +454,17 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
                                                                 gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
                                                                 xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+    if (gate.trace) {  // profiling: the whole workgroup's span (vector stores)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+            unsigned long long* t = gate.trace + 3ull * blockIdx.x;
+            t[0] = t_start;
+            t[1] = wall_clock64();
+            t[2] = ((unsigned long long)r << 40) | ((unsigned long long)(xcc & 0xff) << 32) | hw;
+        }
+    }
 }
 
 // Chunk rule for the pipelined pass, in workgroup tasks: a whole number of
@@ -461,8 +474,13 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
 // resident: 13 chunks of 1261 rows = 962 tasks, not 14 = 1036). Thin regions
 // (border strips) use ~1024 tasks. CME_PIPE_CHUNK / CME_PIPE_PER_CU override
 // for sweeps (per_cu = task target per CU).
+// `reserve`: tasks of the thin regions sharing this launch (the fused
+// schedule's border strips, last in the grid). The bulk rule's task count is
+// a whole number of resident rounds, so without the reserve the border tasks
+// formed a partial extra round behind the interior (N = 4 and 8 ranks: the
+// interior is exactly one round); with it they fit in the last round.
 template <int NS, int RB, int VW = 4>
-int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident, bool thin_floor) {
+int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident, bool thin_floor, long reserve = 0) {
     const int env_chunk = (int)cme::tune_get(cme::kTunePipeChunk);
     const int env_per_cu = (int)cme::tune_get(cme::kTunePipePerCU);
     const int thin_min = (int)cme::tune_get(cme::kTunePipeThinMin);
@@ -497,9 +515,11 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
             // (wide lanes, 3 workgroups per CU: 8 per CU at >= 8192 rows,
             // ~280-row chunks at 16384; 6 at >= 4096 rows; profiles/
             // heat_pipe_wide_r3.md)
-            if (per_cu <= 0)
+            if (per_cu <= 0) {
                 tasks = H >= 8192 ? (VW == 8 ? 8L : 14L) * device_cu_count()
                                   : (H >= 4096 ? (VW == 8 ? 6L : 8L) * device_cu_count() : resident);
+                tasks = tasks - reserve < tasks / 2 ? tasks / 2 : tasks - reserve;
+            }
             long per_strip = tasks / strips;
             per_strip = per_strip < 1 ? 1 : per_strip;
             rows = (H + per_strip - 1) / per_strip;
@@ -527,13 +547,27 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
     int tasks = 0;
     const int gate_from = gate.from;
     gate.from = kMaxS2Regions;  // region index in R of the first gated input region
+    constexpr int kOut = PipeOut<NS, WPR, VW, HeatOrder<ORDER>::B>::kOut;
+    // tasks of the thin regions (see pipe_chunk's reserve)
+    long reserve = 0;
+    if (n > 1) {
+        const long lo = 4 * RB > 16 ? 4 * RB : 16;
+        for (int i = 0; i < n; ++i) {
+            const Region& g = gs[i];
+            const int H = g.ye - g.yb;
+            if (H <= 0 || g.xe <= g.xb) continue;
+            const int strips = (int)cdiv(g.xe - (g.xb & ~(VW - 1)), kOut);
+            if ((long)strips * cdiv(H, lo) < 1024)
+                reserve += (long)strips * cdiv(H, pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, true));
+        }
+    }
     for (int i = 0; i < n; ++i) {
         const Region& g = gs[i];
         const int H = g.ye - g.yb;
         if (i >= gate_from && gate.from == kMaxS2Regions) gate.from = R.n;
         if (H <= 0 || g.xe <= g.xb) continue;
-        const int strips = (int)cdiv(g.xe - (g.xb & ~(VW - 1)), PipeOut<NS, WPR, VW, HeatOrder<ORDER>::B>::kOut);
-        const int chunk = pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, n > 1);
+        const int strips = (int)cdiv(g.xe - (g.xb & ~(VW - 1)), kOut);
+        const int chunk = pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, n > 1, reserve);
         const int k = R.n++;
         R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
         R.strips[k] = strips;

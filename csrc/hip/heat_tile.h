@@ -1,0 +1,174 @@
+// LDS-resident tile pass (see heat_tile.hip for the design notes).
+#pragma once
+
+#include "cme213/common.h"
+#include "cme213/heat_region.h"
+#include "cme213/heat_stencil.h"
+
+namespace cme_tile {
+
+using namespace cme;
+
+template <typename T>
+struct alignas(2 * sizeof(T)) Pair {
+    T v[2];
+};
+
+template <typename T, int ORDER, int NS, int TX, int TY>
+struct TileGeom {
+    static constexpr int B = HeatOrder<ORDER>::B;
+    static constexpr int H = NS * B;
+    static constexpr int LW = TX + 2 * H;  // LDS row: TX + 2H values (TX, H even for B >= 2)
+    static constexpr int PW = LW + (LW & 1);
+    static constexpr int LH = TY + 2 * H;
+    static constexpr size_t kBytes = 2ull * LH * PW * sizeof(T);
+    static_assert(TX % 2 == 0, "column pairs");
+};
+
+// One timestep of the tile: rows [r_lo, r_hi) x columns [c_lo, c_hi) (LDS
+// coordinates) from src into dst.
+template <typename T, int ORDER, bool FMA, int PW, int NT>
+__device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restrict__ dst, int c_lo, int c_hi, int r_lo,
+                                          int r_hi, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int WIN = 2 * B + 1;
+    constexpr int NXP = (B + 1) / 2;  // x-neighbour pairs on each side
+    if (c_hi <= c_lo || r_hi <= r_lo) return;
+    const int ca = c_lo & ~1;
+    const int npairs = (c_hi - ca + 1) >> 1;
+    int nb = NT / npairs;
+    nb = nb < 1 ? 1 : nb;
+    const int rows = r_hi - r_lo;
+    const int R = (rows + nb - 1) / nb;
+    for (int task = threadIdx.x; task < npairs * nb; task += NT) {
+        const int band = task / npairs;
+        const int c0 = ca + 2 * (task - band * npairs);
+        const int rb = r_lo + band * R;
+        const int re = min(r_hi, rb + R);
+        if (rb >= re) continue;
+        const bool w0 = c0 >= c_lo, w1 = c0 + 1 < c_hi;
+        const Pair<T>* s2 = reinterpret_cast<const Pair<T>*>(src);
+        Pair<T>* d2 = reinterpret_cast<Pair<T>*>(dst);
+        const int cp = c0 >> 1;  // pair column
+        // window: rows rb-B .. rb+B; slot (row - (rb - B)) % WIN
+        Pair<T> win[WIN];
+#pragma unroll
+        for (int k = 0; k < 2 * B; ++k) win[k] = s2[(rb - B + k) * (PW / 2) + cp];
+        for (int r0 = rb; r0 < re; r0 += WIN) {
+#pragma unroll
+            for (int u = 0; u < WIN; ++u) {
+                const int r = r0 + u;
+                if (r < re) {
+                    // row r + B enters slot (u + 2B) % WIN; the centre row r is slot (u + B) % WIN
+                    win[(u + 2 * B) % WIN] = s2[(r + B) * (PW / 2) + cp];
+                    Pair<T> xl[NXP], xr[NXP];
+#pragma unroll
+                    for (int q = 0; q < NXP; ++q) {
+                        xl[q] = s2[r * (PW / 2) + cp - 1 - q];  // columns c0-2-2q, c0-1-2q
+                        xr[q] = s2[r * (PW / 2) + cp + 1 + q];  // columns c0+2+2q, c0+3+2q
+                    }
+                    const Pair<T> c = win[(u + B) % WIN];
+                    T out[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+                        for (int k = 0; k < B; ++k) {
+                            // x of column c0 + j - (k + 1) and c0 + j + (k + 1)
+                            const int dm = j - (k + 1), dp = j + (k + 1);  // offsets from c0
+                            xm[k] = dm >= 0 ? c.v[dm] : xl[(-dm - 1) / 2].v[1 - ((-dm - 1) & 1)];
+                            xp[k] = dp <= 1 ? c.v[dp] : xr[(dp - 2) / 2].v[(dp - 2) & 1];
+                            ym[k] = win[(u + B - (k + 1)) % WIN].v[j];
+                            yp[k] = win[(u + B + (k + 1)) % WIN].v[j];
+                        }
+                        out[j] = heat_update_sel<ORDER, FMA>(c.v[j], xm, xp, ym, yp, xcfl, ycfl);
+                    }
+                    if (w0 && w1) {
+                        Pair<T> o;
+                        o.v[0] = out[0];
+                        o.v[1] = out[1];
+                        d2[r * (PW / 2) + cp] = o;
+                    } else {
+                        if (w0) dst[r * PW + c0] = out[0];
+                        if (w1) dst[r * PW + c0 + 1] = out[1];
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
+__global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
+                                                       int gy, Region g, int tiles_x, T xcfl, T ycfl) {
+    using G = TileGeom<T, ORDER, NS, TX, TY>;
+    constexpr int B = G::B, H = G::H, PW = G::PW, LW = G::LW, LH = G::LH;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    T* L0 = reinterpret_cast<T*>(smem);
+    T* L1 = L0 + LH * PW;
+    const int tyi = (int)blockIdx.x / tiles_x;
+    const int txi = (int)blockIdx.x - tyi * tiles_x;
+    const int ox = g.xb + txi * TX, oy = g.yb + tyi * TY;  // output origin (grid)
+    const int gx0 = ox - H, gy0 = oy - H;                  // LDS (0, 0) in grid coordinates
+    // tile + halo into both buffers (cells outside the grid buffer are never
+    // read by a point inside g: the ghost layer stops every cone). Loads in
+    // batches of kLB per thread, all issued before their LDS stores, so the
+    // memory latency is paid once per batch, not once per element.
+    constexpr int kN = LH * LW;
+    constexpr int kLB = 8;
+    for (int i0 = 0; i0 < kN; i0 += NT * kLB) {
+        T v[kLB];
+#pragma unroll
+        for (int k = 0; k < kLB; ++k) {
+            const int i = i0 + k * NT + (int)threadIdx.x;
+            const int r = i / LW, c = i - r * LW;
+            const int x = gx0 + c, y = gy0 + r;
+            v[k] = (i < kN && x >= 0 && x < pitch && y >= 0 && y < gy) ? prev[(size_t)y * pitch + x] : T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < kLB; ++k) {
+            const int i = i0 + k * NT + (int)threadIdx.x;
+            if (i < kN) {
+                const int r = i / LW, c = i - r * LW;
+                L0[r * PW + c] = v[k];
+                L1[r * PW + c] = v[k];
+            }
+        }
+    }
+    __syncthreads();
+    // region g in LDS coordinates
+    const int gxl = g.xb - gx0, gxh = g.xe - gx0, gyl = g.yb - gy0, gyh = g.ye - gy0;
+#pragma unroll
+    for (int s = 1; s <= NS; ++s) {
+        const int e = (NS - s) * B;  // this step's reach beyond the output tile
+        const int c_lo = max(H - e, gxl), c_hi = min(H + TX + e, gxh);
+        const int r_lo = max(H - e, gyl), r_hi = min(H + TY + e, gyh);
+        tile_step<T, ORDER, FMA, PW, NT>((s & 1) ? L0 : L1, (s & 1) ? L1 : L0, c_lo, c_hi, r_lo, r_hi, xcfl, ycfl);
+        __syncthreads();
+    }
+    const T* fin = (NS & 1) ? L1 : L0;
+    const int c_lo = max(H, gxl), c_hi = min(H + TX, gxh);
+    const int r_lo = max(H, gyl), r_hi = min(H + TY, gyh);
+    const int w = c_hi - c_lo;
+    if (w <= 0 || r_hi <= r_lo) return;
+    for (int i = threadIdx.x; i < w * (r_hi - r_lo); i += NT) {
+        const int r = r_lo + i / w, c = c_lo + i % w;
+        curr[(size_t)(gy0 + r) * pitch + gx0 + c] = fin[r * PW + c];
+    }
+}
+
+template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
+int launch_tile(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, hipStream_t s) {
+    using G = TileGeom<T, ORDER, NS, TX, TY>;
+    auto k = heat_tile_kernel<T, ORDER, NS, FMA, TX, TY, NT>;
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::kBytes);
+    if (attr != hipSuccess) return (int)attr;
+    const int W = g.xe - g.xb, Hh = g.ye - g.yb;
+    if (W <= 0 || Hh <= 0) return 0;
+    const int tx = (W + TX - 1) / TX, ty = (Hh + TY - 1) / TY;
+    hipLaunchKernelGGL(k, dim3(tx * ty), dim3(NT), G::kBytes, s, prev, curr, pitch, gy, g, tx, xcfl, ycfl);
+    return (int)hipGetLastError();
+}
+
+}  // namespace cme_tile

@@ -112,3 +112,27 @@ CME_EXPORT int cme_heat_pipe_tune(const float* prev, float* curr, int pitch, int
         default: return (int)hipErrorInvalidValue;
     }
 }
+
+// Profiling entry (benchmarks/trace_pipe_tasks.py): the production fp32
+// wide-lane pass (FMA, term-major chains, RB 2) over `nout` regions as the
+// fused distributed schedule launches them (deep interior first, then the
+// border strips), with every workgroup recording {start, end} wall-clock
+// ticks and {region << 40 | XCC_ID << 32 | HW_ID} into trace (3 x u64 per
+// workgroup; the caller sizes it for the grid and zeroes it). chunk /
+// per_cu: the chunk rule's overrides (0 = production rule).
+CME_EXPORT int cme_heat_pipe_trace(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                   const int* ext, int ns, float xcfl, float ycfl, int chunk, int per_cu,
+                                   unsigned long long* trace, void* stream) {
+    Region gs[kMaxS2Regions];
+    if (nout < 1 || nout > kMaxS2Regions || !trace) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < nout; ++i) gs[i] = Region{out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]};
+    const Region e{ext[0], ext[1], ext[2], ext[3]};
+    PipeGate gate;
+    gate.trace = trace;
+    hipStream_t s = as_stream(stream);
+    switch (ns) {
+        case 3: return launch_pipe_multi<float, 8, 3, 4, 2, 1, true, 1, 8>(prev, curr, pitch, gy, gs, nout, e, xcfl, ycfl, chunk, per_cu, s, gate);
+        case 4: return launch_pipe_multi<float, 8, 4, 4, 2, 1, true, 1, 8>(prev, curr, pitch, gy, gs, nout, e, xcfl, ycfl, chunk, per_cu, s, gate);
+        default: return (int)hipErrorInvalidValue;
+    }
+}

@@ -53,6 +53,9 @@ struct PipeGate {
     int from = 0;
     unsigned* timeout = nullptr;
     unsigned spins = 1u << 24;
+    // profiling only (hip_tune/heat_pipe_tune.hip cme_heat_pipe_trace): per
+    // task {start, end} wall clock (100 MHz) and {HW_ID, XCC_ID, region}
+    unsigned long long* trace = nullptr;
 };
 
 }  // namespace cme
