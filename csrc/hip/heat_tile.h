@@ -51,21 +51,36 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
         Pair<T>* d2 = reinterpret_cast<Pair<T>*>(dst);
         const int cp = c0 >> 1;  // pair column
         // window: rows rb-B .. rb+B; slot (row - (rb - B)) % WIN
+        const int P = PW / 2;  // pairs per LDS row
         Pair<T> win[WIN];
 #pragma unroll
-        for (int k = 0; k < 2 * B; ++k) win[k] = s2[(rb - B + k) * (PW / 2) + cp];
+        for (int k = 0; k < 2 * B; ++k) win[k] = s2[(rb - B + k) * P + cp];
+        // software pipeline: row r's LDS words (the window row r + B and the
+        // x-neighbour pairs of row r) are loaded while row r - 1 computes
+        Pair<T> nw = s2[(rb + B) * P + cp];
+        Pair<T> nxl[NXP], nxr[NXP];
+#pragma unroll
+        for (int q = 0; q < NXP; ++q) {
+            nxl[q] = s2[rb * P + cp - 1 - q];  // columns c0-2-2q, c0-1-2q
+            nxr[q] = s2[rb * P + cp + 1 + q];  // columns c0+2+2q, c0+3+2q
+        }
         for (int r0 = rb; r0 < re; r0 += WIN) {
 #pragma unroll
             for (int u = 0; u < WIN; ++u) {
                 const int r = r0 + u;
                 if (r < re) {
                     // row r + B enters slot (u + 2B) % WIN; the centre row r is slot (u + B) % WIN
-                    win[(u + 2 * B) % WIN] = s2[(r + B) * (PW / 2) + cp];
+                    win[(u + 2 * B) % WIN] = nw;
                     Pair<T> xl[NXP], xr[NXP];
 #pragma unroll
-                    for (int q = 0; q < NXP; ++q) {
-                        xl[q] = s2[r * (PW / 2) + cp - 1 - q];  // columns c0-2-2q, c0-1-2q
-                        xr[q] = s2[r * (PW / 2) + cp + 1 + q];  // columns c0+2+2q, c0+3+2q
+                    for (int q = 0; q < NXP; ++q) xl[q] = nxl[q], xr[q] = nxr[q];
+                    if (r + 1 < re) {
+                        nw = s2[(r + 1 + B) * P + cp];
+#pragma unroll
+                        for (int q = 0; q < NXP; ++q) {
+                            nxl[q] = s2[(r + 1) * P + cp - 1 - q];
+                            nxr[q] = s2[(r + 1) * P + cp + 1 + q];
+                        }
                     }
                     const Pair<T> c = win[(u + B) % WIN];
                     T out[2];
@@ -87,7 +102,7 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
                         Pair<T> o;
                         o.v[0] = out[0];
                         o.v[1] = out[1];
-                        d2[r * (PW / 2) + cp] = o;
+                        d2[r * P + cp] = o;
                     } else {
                         if (w0) dst[r * PW + c0] = out[0];
                         if (w1) dst[r * PW + c0 + 1] = out[1];
