@@ -34,7 +34,8 @@ def heat2d_mpi_main(argv=None) -> int:
     ap.add_argument("--device", default=None)
     ap.add_argument("--float", action="store_true", help="fp32 instead of the reference's fp64")
     ap.add_argument("--tblock", default="auto", help="timesteps per halo exchange / HBM pass (1-4, or auto)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "pipe", "streamn"], help="3-4 step pass kernel")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "pipe", "streamn", "tile"],
+                    help="multi-step pass kernel (tile: LDS-resident tiles, single-grid runs)")
     ap.add_argument("--fma", action="store_true", help="FMA-contracted stencil (the reference CPU's is not)")
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
                     help="GPU time loop: the native C++ loop after a bitwise self-test (auto), required (on), "

@@ -139,9 +139,14 @@ _OPP = {"top": "bottom", "bottom": "top", "left": "right", "right": "left"}
 # vs pipe4 0.0085 -- profiles/heat_fp64_pipe_r2.jsonl, heat_fp64_stream3_r2.jsonl,
 # dist_fused_r2.md)
 _F64_PIPE_MIN_POINTS = 2000 * 2000
+# single-grid fp64 runs up to this size use the LDS-resident tile pass
+# (csrc/hip/heat_tile.hip, four steps per pass): 1000^2 order 8, 1000 steps,
+# 4.63 ms FMA / 5.35 exact vs 5.67 / 6.88 for streamN; at 2000^2 the pipelined
+# pass wins (8.5 vs 15.5 ms; profiles/heat_tile_r4.md)
+_F64_TILE_MAX_POINTS = 1200 * 1200
 
 
-def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda") -> int:
+def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool = False) -> int:
     """Timesteps per HBM pass (and per halo exchange) for a subdomain of
     ``points`` cells: 4 for fp32 (pipelined pass, every N of the 16384^2
     bench) and for large fp64 subdomains; 3 (FMA) or 2 (exact) for small fp64
@@ -151,13 +156,18 @@ def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda") -> int:
         return 1
     if dtype == torch.float32 or points >= _F64_PIPE_MIN_POINTS:
         return 4
+    if solo and points <= _F64_TILE_MAX_POINTS:
+        return 4  # the tile pass (auto_kernel)
     return 3 if fma else 2
 
 
-def auto_kernel(dtype, points: int, tblock: int) -> str:
+def auto_kernel(dtype, points: int, tblock: int, solo: bool = False) -> str:
     """Pass kernel for 3-4 step passes: the wave-pipelined pass for fp32 and
     for fp64 subdomains of at least 2000^2 cells (and every fp64 4-step pass:
-    streamN stops at 3 for doubles), streamN below that."""
+    streamN stops at 3 for doubles), streamN below that; a small fp64 grid on
+    one GPU with no neighbours (``solo``) runs the LDS-resident tile pass."""
+    if solo and dtype == torch.float64 and points <= _F64_TILE_MAX_POINTS and tblock >= 2:
+        return "tile"
     if tblock < 3:
         return "streamn"
     if dtype == torch.float32 or tblock > 3 or points >= _F64_PIPE_MIN_POINTS:
@@ -251,15 +261,18 @@ class DistHeat:
             pts = max(b.nx * b.ny for b in (decompose(params.nx, params.ny, self.world, params.grid_method, r,
                                                       self.periodic)
                                             for r in range(self.world)))
+            solo = self.world == 1 and not any(self.periodic)
             if tblock == "auto":
-                tblock = auto_tblock(dtype, pts, fma, torch.device(device).type)
+                tblock = auto_tblock(dtype, pts, fma, torch.device(device).type, solo)
             if kernel == "auto":
-                kernel = auto_kernel(dtype, pts, tblock)
+                kernel = auto_kernel(dtype, pts, tblock, solo and torch.device(device).type == "cuda")
         if tblock not in (1, 2, 3, 4):
             raise ValueError("tblock must be 1..4")
-        if kernel not in ("streamn", "pipe"):
-            raise ValueError("kernel must be 'streamn' or 'pipe'")
-        if tblock > 3 and dtype == torch.float64 and kernel != "pipe" and torch.device(device).type == "cuda":
+        if kernel not in ("streamn", "pipe", "tile"):
+            raise ValueError("kernel must be 'streamn', 'pipe' or 'tile'")
+        if kernel == "tile" and (self.world != 1 or any(self.periodic)):
+            raise ValueError("kernel='tile' runs single-grid (world 1, non-periodic) passes only")
+        if tblock > 3 and dtype == torch.float64 and kernel == "streamn" and torch.device(device).type == "cuda":
             raise ValueError("fp64 4-step passes need kernel='pipe' on the GPU (streamN fp64 stops at 3)")
         self.fma = bool(fma)
         # 3-4 step passes: streamN (one wave holds every step) or the
@@ -652,6 +665,8 @@ class DistHeat:
         if self.tblock == 1:
             return self.variant
         suffix = "_fma" if self.fma else ""
+        if self.kernel == "tile":
+            return f"tile{self.tblock}" + suffix
         if self.tblock == 2:
             return "stream2" + suffix
         return ("pipe" if self.kernel == "pipe" else "stream") + str(self.tblock) + suffix

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kernel", default="streamn", choices=["streamn", "pipe"],
                     help="3-4 step pass kernel: streamN or the wave-pipelined pass")
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="tuning knobs name=value (cme213x.utils.tuning), e.g. pipe_per_cu=6 pipe_vw=4")
     args = ap.parse_args()
     import torch
 
@@ -51,6 +53,11 @@ def main():
         def barrier(self):
             pass
 
+    from cme213x.utils import tuning
+
+    knobs = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
+    for k, v in knobs.items():
+        tuning.set(k, v)
     base = None
     for w in args.world:
         rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
@@ -77,7 +84,7 @@ def main():
         ms = sorted(times)[len(times) // 2]
         base = base or ms * w
         print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
-                          "kernel": args.kernel,
+                          "kernel": args.kernel, "tune": knobs,
                           "reps": args.reps,
                           "ms_per_step": round(ms, 4),
                           "compute_scaling_eff": round(base / (ms * w), 3)}), flush=True)

@@ -28,6 +28,8 @@ def main() -> int:
     ap.add_argument("--windows", type=int, default=8)
     ap.add_argument("--steps", type=int, default=60, help="timesteps per window (a multiple of 60 suits 3/4/5/6)")
     ap.add_argument("--spin", type=float, default=0.5)
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="tuning knobs name=value[/value...] (cme213x.utils.tuning); one run per value combination")
     args = ap.parse_args()
     import torch
 
@@ -51,37 +53,48 @@ def main() -> int:
         out = heat_run(a, b, g.interior, g.order, g.xcfl, g.ycfl, k, v)
         g.cur = g.cur if out is a else 1 - g.cur
 
+    from cme213x.utils import tuning
+    import itertools
+
+    knob_vals = [[(kv.split("=")[0], int(v)) for v in kv.split("=")[1].split("/")] for kv in args.tune]
+    combos = list(itertools.product(*knob_vals)) if knob_vals else [()]
     variants = args.variants.split(",")
     t_end = time.perf_counter() + args.spin
     while time.perf_counter() < t_end:
         for v in variants:
             run(v, 12)
         torch.cuda.synchronize()
-    finals = {}
-    for data in args.data.split(","):
-        for v in variants:
-            g.buf.copy_(init[data])
-            g.cur = 0
-            run(v, 12)  # warm-up on this data
-            torch.cuda.synchronize()
-            g.buf.copy_(init[data])
-            g.cur = 0
-            win = []
-            for _ in range(args.windows):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                run(v, args.steps)
-                e1.record()
-                e1.synchronize()
-                win.append(e0.elapsed_time(e1) / args.steps)
-            finals[(data, v)] = g.buf[g.cur].clone()
-            same = None
-            if v != "pipe4_fma" and (data, "pipe4_fma") in finals:
-                same = bool(torch.equal(finals[(data, v)], finals[(data, "pipe4_fma")]))
-            print(json.dumps({"bench": "heat_ic", "n": args.n, "variant": v, "data": data,
-                              "ms_per_step_windows": [round(x, 4) for x in win],
-                              "ms_per_step_median": round(statistics.median(win), 4),
-                              "ms_per_step_first": round(win[0], 4), "bitwise_vs_pipe4": same}), flush=True)
+    for combo in combos:
+        for k, v in combo:
+            tuning.set(k, v)
+        knobs = {k: v for k, v in combo}
+        finals = {}
+        for data in args.data.split(","):
+            for v in variants:
+                g.buf.copy_(init[data])
+                g.cur = 0
+                run(v, 12)  # warm-up on this data
+                torch.cuda.synchronize()
+                g.buf.copy_(init[data])
+                g.cur = 0
+                win = []
+                for _ in range(args.windows):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    run(v, args.steps)
+                    e1.record()
+                    e1.synchronize()
+                    win.append(e0.elapsed_time(e1) / args.steps)
+                finals[(data, v)] = g.buf[g.cur].clone()
+                same = None
+                if v != "pipe4_fma" and (data, "pipe4_fma") in finals:
+                    same = bool(torch.equal(finals[(data, v)], finals[(data, "pipe4_fma")]))
+                print(json.dumps({"bench": "heat_ic", "n": args.n, "variant": v, "data": data, "tune": knobs,
+                                  "ms_per_step_windows": [round(x, 4) for x in win],
+                                  "ms_per_step_median": round(statistics.median(win), 4),
+                                  "ms_per_step_first": round(win[0], 4), "bitwise_vs_pipe4": same}), flush=True)
+        for k, _ in combo:
+            tuning.reset(k)
     return 0
 
 

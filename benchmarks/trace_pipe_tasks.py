@@ -29,6 +29,7 @@ def main() -> int:
     ap.add_argument("--per-cu", type=int, default=0)
     ap.add_argument("--slots", type=int, default=3, help="resident workgroups per CU (occupancy)")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dump", default="", help="path prefix: save the median rep's raw spans (npz)")
     args = ap.parse_args()
     import ctypes
 
@@ -84,9 +85,9 @@ def main() -> int:
             t0 = t[:, 0].min()
             start, end = (t[:, 0] - t0) * 10.0 / 1e3, (t[:, 1] - t0) * 10.0 / 1e3  # us (100 MHz)
             region = (t[:, 2] >> 40).astype(int)
-            spans.append((float(end.max()), start, end, region))
+            spans.append((float(end.max()), start, end, region, (t[:, 2] & 0xFFFFFFFF), (t[:, 2] >> 32) & 0xFF))
         spans.sort(key=lambda x: x[0])
-        kspan, start, end, region = spans[len(spans) // 2]
+        kspan, start, end, region, hwid, xcc = spans[len(spans) // 2]
         dur = end - start
         per_region = {}
         for r in sorted(set(region.tolist())):
@@ -95,6 +96,9 @@ def main() -> int:
                 "tasks": int(d.size), "median_us": round(float(np.median(d)), 2),
                 "p90_us": round(float(np.percentile(d, 90)), 2), "rows": int(regs[r, 3] - regs[r, 2])}
         util = float(dur.sum()) / (ncu * args.slots * kspan)
+        if args.dump:
+            os.makedirs(os.path.dirname(args.dump) or ".", exist_ok=True)
+            np.savez(f"{args.dump}_w{world}.npz", start=start, end=end, region=region, hw=hwid, xcc=xcc)
         rec = {"bench": "pipe_task_trace", "world": world, "rank": rank, "tblock": args.tblock,
                "chunk": args.chunk, "per_cu": args.per_cu, "kernel_span_us": round(kspan, 2),
                "tasks": int(dur.size), "regions": per_region,

@@ -474,11 +474,12 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
 // resident: 13 chunks of 1261 rows = 962 tasks, not 14 = 1036). Thin regions
 // (border strips) use ~1024 tasks. CME_PIPE_CHUNK / CME_PIPE_PER_CU override
 // for sweeps (per_cu = task target per CU).
-// `reserve`: tasks of the thin regions sharing this launch (the fused
-// schedule's border strips, last in the grid). The bulk rule's task count is
-// a whole number of resident rounds, so without the reserve the border tasks
-// formed a partial extra round behind the interior (N = 4 and 8 ranks: the
-// interior is exactly one round); with it they fit in the last round.
+// `reserve` < 0: take that many tasks off the bulk rule (so that the thin
+// regions sharing the launch -- the fused schedule's border strips, last in
+// the grid -- fit in the bulk's last round of resident workgroups). Measured
+// on one N = 4 / 8 rank (profiles/dist_rank_trace_r4.md): every task then
+// starts at once, but the pass got 5 / 2 % SLOWER (the span is set by the
+// slowest interior tasks, which got taller), so launch_pipe_multi passes 0.
 template <int NS, int RB, int VW = 4>
 int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident, bool thin_floor, long reserve = 0) {
     const int env_chunk = (int)cme::tune_get(cme::kTunePipeChunk);
@@ -518,7 +519,7 @@ int pipe_chunk(int strips, int H, int chunk_hint, int per_cu_hint, long resident
             if (per_cu <= 0) {
                 tasks = H >= 8192 ? (VW == 8 ? 8L : 14L) * device_cu_count()
                                   : (H >= 4096 ? (VW == 8 ? 6L : 8L) * device_cu_count() : resident);
-                tasks = tasks - reserve < tasks / 2 ? tasks / 2 : tasks - reserve;
+                if (reserve < 0) tasks = tasks + reserve < tasks / 2 ? tasks / 2 : tasks + reserve;
             }
             long per_strip = tasks / strips;
             per_strip = per_strip < 1 ? 1 : per_strip;
@@ -548,19 +549,7 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
     const int gate_from = gate.from;
     gate.from = kMaxS2Regions;  // region index in R of the first gated input region
     constexpr int kOut = PipeOut<NS, WPR, VW, HeatOrder<ORDER>::B>::kOut;
-    // tasks of the thin regions (see pipe_chunk's reserve)
-    long reserve = 0;
-    if (n > 1) {
-        const long lo = 4 * RB > 16 ? 4 * RB : 16;
-        for (int i = 0; i < n; ++i) {
-            const Region& g = gs[i];
-            const int H = g.ye - g.yb;
-            if (H <= 0 || g.xe <= g.xb) continue;
-            const int strips = (int)cdiv(g.xe - (g.xb & ~(VW - 1)), kOut);
-            if ((long)strips * cdiv(H, lo) < 1024)
-                reserve += (long)strips * cdiv(H, pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, true));
-        }
-    }
+    const long reserve = 0;  // see pipe_chunk
     for (int i = 0; i < n; ++i) {
         const Region& g = gs[i];
         const int H = g.ye - g.yb;

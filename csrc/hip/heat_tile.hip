@@ -6,7 +6,7 @@
 // grid has 2-5 such strips, so filling 1024 SIMDs means chunks of a handful
 // of rows, each paying 2(NS-1)B warm-up rows -- the pass is latency- and
 // recompute-bound at ~17 us for three steps (profiles/hw5_default_path_r3.jsonl)
-// while its arithmetic is ~1.5 us. Here a 512-thread workgroup owns a 2-D
+// while its arithmetic is ~1.5 us. Here a 1024-thread workgroup owns a 2-D
 // output tile (64 x TY points): it loads the tile plus an NS*B-deep halo into
 // LDS ONCE, runs NS timesteps entirely in LDS (each step over a region B
 // narrower per side than the one before -- the dependency cone), and writes
@@ -27,7 +27,7 @@ using namespace cme;
 
 namespace {
 
-constexpr int kTileThreads = 512;
+constexpr int kTileThreads = 1024;  // 16 waves: 4 per SIMD (tune_tile.py cfg 2)
 
 // Tile shapes: fp64 64 x 64 (1000^2 = 256 tiles, one workgroup per CU; LDS
 // 2 x (64 + 2NSB)^2 x 8 B = 102 / 124 / 147 KB at NS = 2 / 3 / 4); fp32

@@ -64,3 +64,37 @@ def test_tile_variants_refuse_single_step_api():
     with pytest.raises(ValueError):
         heat_step(g.buf[0], g.buf[1], g.interior, 8, g.xcfl, g.ycfl, "tile2")
     assert np.isfinite(g.state()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fma", [False, True])
+def test_hw5_default_path_uses_tile_pass(gpu, fma):
+    """The hw5 driver's automatic choice on a small single-grid fp64 run is the
+    tile pass (four steps per pass), bitwise equal to the CPU oracle's single
+    steps (exact or FMA) -- the reference's 1000^2 shape, 13 steps (three
+    passes and a one-step tail)."""
+    from cme213x.models.heat2d_dist import DistHeat
+
+    p = SimParams(nx=1000, ny=1000, order=8, iters=13, ic=3.0, bc=(0.0, 10.0, 0.0, 10.0), flavor="hw5")
+    sim = DistHeat(p, None, torch.float64, gpu, tblock="auto", kernel="auto", fma=fma)
+    assert sim.kernel == "tile" and sim.tblock == 4 and sim.solo()
+    ref = DistHeat(p, None, torch.float64, "cpu", variant="naive", fma=fma)
+    for d in (sim, ref):
+        (s,) = d.subs.values()
+        g, H = s.grid, s.grid.H
+        yy, xx = np.meshgrid(np.arange(1000), np.arange(1000), indexing="ij")
+        g.buf[:, H:H + 1000, H:H + 1000] = torch.from_numpy(np.sin(0.01 * xx) * np.cos(0.02 * yy) + 3.0).to(g.device)
+    sim.run(13)
+    ref.run(13)
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
+
+
+def test_tile_kernel_only_for_single_grids():
+    from cme213x.models.heat2d_dist import DistHeat
+
+    p = SimParams(nx=100, ny=100, order=8, iters=2, flavor="hw5")
+    with pytest.raises(ValueError, match="tile"):
+        DistHeat(p, None, torch.float64, "cpu", tblock=4, kernel="tile", local_ranks=[0, 1], world=2)
+    with pytest.raises(ValueError, match="tile"):
+        DistHeat(p, None, torch.float64, "cpu", tblock=4, kernel="tile", periodic=(False, True))
