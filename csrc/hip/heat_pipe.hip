@@ -80,22 +80,9 @@ namespace {
 template <int ORDER, bool FMA>
 int pipe_ns_f64(const double* p, double* c, int pitch, int gy, const Region* gs, int n, Region e, int ns, double xcfl,
                 double ycfl, int chunk, hipStream_t s, PipeGate gate) {
-    // CME_PIPE_TM64=1: issue the FMA chains of a lane's 4 points term by term
-    // (bitwise the same; the fp32 wide pass's order). Off by default until
-    // measured on the fp64 shapes (the round-3 session ran out of GPU boxes).
-    static const bool tm = [] {
-        const char* e = getenv("CME_PIPE_TM64");
-        return e && atoi(e) == 1;
-    }();
-    if constexpr (FMA) {
-        if (tm) {
-            switch (ns) {
-                case 3: return launch_pipe_multi<double, ORDER, 3, 4, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
-                case 4: return launch_pipe_multi<double, ORDER, 4, 4, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
-                default: return (int)hipErrorInvalidValue;
-            }
-        }
-    }
+    // (a term-major chain order, the fp32 wide pass's, was measured here on
+    // the hw5 shapes: 1000^2 / 2000^2 / 4000^2, orders 4 and 8, within 1 %
+    // of this chain-major order -- profiles/heat_tile_r4.md -- and removed)
     switch (ns) {
         case 3: return launch_pipe_multi<double, ORDER, 3, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
         case 4: return launch_pipe_multi<double, ORDER, 4, FMA, 2, 1, false>(p, c, pitch, gy, gs, n, e, xcfl, ycfl, chunk, 0, s, gate);
