@@ -246,6 +246,23 @@ def main() -> int:
     # random-init inputs"): uniform(0, 10) interior, seeded per rank, same
     # BCs. The pass is issue/power bound, and random data toggles more bits
     # than the reference's uniform IC, so this is the slower figure.
+    # N = 1: the distributed native schedule (cme_heat_dist_run, the loop the
+    # N > 1 points run, exchange off) on the same grid and the same uniform
+    # initial field, so the N = 1 point of a scaling curve can be read
+    # against the same schedule
+    secs_dist1 = None
+    if on_gpu and comm.size == 1 and args.kernel == "pipe":
+        for s in sim.subs.values():
+            s.grid.buf.copy_(init_state[(s.blk.x0, s.blk.y0)])
+        run_d = lambda k: sim.run_native(k, transport=2)  # noqa: E731
+        run_d(args.warmup)
+        sync()
+        t0 = time.perf_counter()
+        run_d(args.steps)
+        sync()
+        secs_dist1 = time.perf_counter() - t0
+        sim.gate_check()
+
     # The same spin-up as the uniform run, on the random field (the power
     # controller settles to the data's switching activity over ~10 ms: a
     # 20-step window right after the switch from the uniform field ran 0.20
@@ -275,20 +292,6 @@ def main() -> int:
         sync()
         secs_random = timed(args.steps)
         sanity_ok = sanity_ok and sane()
-
-    # N = 1: the distributed native schedule (cme_heat_dist_run, the loop the
-    # N > 1 points run, exchange off) on the same grid, so the N = 1 point of
-    # a scaling curve can be read against the same schedule
-    secs_dist1 = None
-    if on_gpu and comm.size == 1 and args.kernel == "pipe":
-        run_d = lambda k: sim.run_native(k, transport=2)  # noqa: E731
-        run_d(args.warmup)
-        sync()
-        t0 = time.perf_counter()
-        run_d(args.steps)
-        sync()
-        secs_dist1 = time.perf_counter() - t0
-        sim.gate_check()
 
     if use_native:
         sch = DistHeat.schedule()

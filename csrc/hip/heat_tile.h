@@ -31,7 +31,7 @@ template <typename T, int ORDER, bool FMA, int PW, int NT>
 __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restrict__ dst, int c_lo, int c_hi, int r_lo,
                                           int r_hi, T xcfl, T ycfl) {
     constexpr int B = HeatOrder<ORDER>::B;
-    constexpr int WIN = 2 * B + 1;
+    constexpr int RING = 2 * B + 2;
     constexpr int NXP = (B + 1) / 2;  // x-neighbour pairs on each side
     if (c_hi <= c_lo || r_hi <= r_lo) return;
     const int ca = c_lo & ~1;
@@ -50,39 +50,47 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
         const Pair<T>* s2 = reinterpret_cast<const Pair<T>*>(src);
         Pair<T>* d2 = reinterpret_cast<Pair<T>*>(dst);
         const int cp = c0 >> 1;  // pair column
-        // window: rows rb-B .. rb+B; slot (row - (rb - B)) % WIN
-        const int P = PW / 2;  // pairs per LDS row
-        Pair<T> win[WIN];
+        // Register ring of RING = 2B + 2 row pairs (one more than the
+        // stencil's 2B + 1): row x sits in slot (x - (rb - B)) % RING, and
+        // row r + 1 + B is loaded into the free slot while row r computes;
+        // the x-neighbour pairs are double-buffered by row parity. The row
+        // loop is unrolled by RING (even), so every slot index is a
+        // compile-time constant: no register moves. LDS addresses are one
+        // row pointer plus immediate offsets.
+        constexpr int P = PW / 2;  // pairs per LDS row
+        Pair<T> win[RING];
+        Pair<T> xl[2][NXP], xr[2][NXP];
+        {
+            const Pair<T>* rp = s2 + (rb - B) * P + cp;
 #pragma unroll
-        for (int k = 0; k < 2 * B; ++k) win[k] = s2[(rb - B + k) * P + cp];
-        // software pipeline: row r's LDS words (the window row r + B and the
-        // x-neighbour pairs of row r) are loaded while row r - 1 computes
-        Pair<T> nw = s2[(rb + B) * P + cp];
-        Pair<T> nxl[NXP], nxr[NXP];
+            for (int k = 0; k <= 2 * B; ++k) win[k] = rp[k * P];
+            rp += B * P;  // row rb
 #pragma unroll
-        for (int q = 0; q < NXP; ++q) {
-            nxl[q] = s2[rb * P + cp - 1 - q];  // columns c0-2-2q, c0-1-2q
-            nxr[q] = s2[rb * P + cp + 1 + q];  // columns c0+2+2q, c0+3+2q
+            for (int q = 0; q < NXP; ++q) {
+                xl[0][q] = rp[-1 - q];  // columns c0-2-2q, c0-1-2q
+                xr[0][q] = rp[1 + q];   // columns c0+2+2q, c0+3+2q
+            }
         }
-        for (int r0 = rb; r0 < re; r0 += WIN) {
+        for (int r0 = rb; r0 < re; r0 += RING) {
+            // one base address per RING rows: every load below is base +
+            // a compile-time (non-negative) offset
+            const Pair<T>* base = s2 + (r0 + 1) * P + cp - NXP;
 #pragma unroll
-            for (int u = 0; u < WIN; ++u) {
+            for (int u = 0; u < RING; ++u) {
                 const int r = r0 + u;
                 if (r < re) {
-                    // row r + B enters slot (u + 2B) % WIN; the centre row r is slot (u + B) % WIN
-                    win[(u + 2 * B) % WIN] = nw;
-                    Pair<T> xl[NXP], xr[NXP];
-#pragma unroll
-                    for (int q = 0; q < NXP; ++q) xl[q] = nxl[q], xr[q] = nxr[q];
-                    if (r + 1 < re) {
-                        nw = s2[(r + 1 + B) * P + cp];
+                    if (r + 1 < re) {  // prefetch row r + 1: its x pairs, and row r + 1 + B into the free slot
+                        const Pair<T>* rp = base + u * P;  // pair column c0 / 2 - NXP of row r + 1
+                        win[(u + 1 + 2 * B) % RING] = rp[B * P + NXP];
 #pragma unroll
                         for (int q = 0; q < NXP; ++q) {
-                            nxl[q] = s2[(r + 1) * P + cp - 1 - q];
-                            nxr[q] = s2[(r + 1) * P + cp + 1 + q];
+                            xl[(u + 1) & 1][q] = rp[NXP - 1 - q];
+                            xr[(u + 1) & 1][q] = rp[NXP + 1 + q];
                         }
                     }
-                    const Pair<T> c = win[(u + B) % WIN];
+                    const Pair<T>(&XL)[NXP] = xl[u & 1];
+                    const Pair<T>(&XR)[NXP] = xr[u & 1];
+                    const Pair<T> c = win[(u + B) % RING];
                     T out[2];
 #pragma unroll
                     for (int j = 0; j < 2; ++j) {
@@ -91,10 +99,10 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
                         for (int k = 0; k < B; ++k) {
                             // x of column c0 + j - (k + 1) and c0 + j + (k + 1)
                             const int dm = j - (k + 1), dp = j + (k + 1);  // offsets from c0
-                            xm[k] = dm >= 0 ? c.v[dm] : xl[(-dm - 1) / 2].v[1 - ((-dm - 1) & 1)];
-                            xp[k] = dp <= 1 ? c.v[dp] : xr[(dp - 2) / 2].v[(dp - 2) & 1];
-                            ym[k] = win[(u + B - (k + 1)) % WIN].v[j];
-                            yp[k] = win[(u + B + (k + 1)) % WIN].v[j];
+                            xm[k] = dm >= 0 ? c.v[dm] : XL[(-dm - 1) / 2].v[1 - ((-dm - 1) & 1)];
+                            xp[k] = dp <= 1 ? c.v[dp] : XR[(dp - 2) / 2].v[(dp - 2) & 1];
+                            ym[k] = win[(u + B - (k + 1) + RING) % RING].v[j];
+                            yp[k] = win[(u + B + (k + 1)) % RING].v[j];
                         }
                         out[j] = heat_update_sel<ORDER, FMA>(c.v[j], xm, xp, ym, yp, xcfl, ycfl);
                     }
