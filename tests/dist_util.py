@@ -35,6 +35,19 @@ def _worker(rank, world, port, fn, args, q):
 
 
 def run_ranks(fn, world: int = 2, args=(), timeout: float = 300):
+    """Run fn(rank, world, *args) on `world` spawned gloo ranks; returns the
+    per-rank results. A rendezvous port taken between free_port() and the
+    store's bind (EADDRINUSE: a host-side race, nothing ran) is retried with
+    a fresh port, twice at most."""
+    for attempt in range(3):
+        try:
+            return _run_ranks_once(fn, world, args, timeout)
+        except RuntimeError as e:
+            if "EADDRINUSE" not in str(e) or attempt == 2:
+                raise
+
+
+def _run_ranks_once(fn, world, args, timeout):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
