@@ -7,6 +7,10 @@ GPURUN ?= /usr/local/graft/bin/gpurun
 ifeq ($(DEBUG),1)
 export CME_DEBUG = 1
 endif
+# TUNE=1: also build csrc/hip_tune/ (the A/B tuning arms) into libcme213_tune.so
+ifeq ($(TUNE),1)
+export CME_TUNE = 1
+endif
 
 .PHONY: all build test test-asan test-gpu bench smoke occupancy clean
 
