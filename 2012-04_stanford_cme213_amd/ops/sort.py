@@ -21,6 +21,7 @@ from .. import _ext
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_sort_u32", "ppppqiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_sort", "ppppppqiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_onesweep", "ppppppqiiipqp")
+_ext.proto(_ext.HIP_PROTOS, "cme_radix_lane_order", "i")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort", "ppppppqip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_u32", "ppqii")
@@ -85,6 +86,15 @@ def _onesweep_ws(keys: torch.Tensor) -> tuple[torch.Tensor, int]:
         e = 1
     _os_epochs[k] = e
     return t, e
+
+
+def radix_lane_order(check: bool = True) -> bool:
+    """Whether the current device resolves the same-address lanes of one
+    returning LDS atomic in lane order -- the property the radix downsweep's
+    lane-atomic ranks rely on (``csrc/hip/sort.hip`` kRankLanes). ``check``
+    runs the library's one-time probe kernel if this device has not been
+    checked yet; the radix sort falls back to ballot-match ranks otherwise."""
+    return bool(_ext._fn("hip", "cme_radix_lane_order")(1 if check else 0))
 
 
 def _merge(keys: torch.Tensor, values: torch.Tensor | None):

@@ -196,34 +196,44 @@ def main() -> int:
     # code object (~5 ms with the GPU idle), after which the clocks take ~10 ms
     # to recover -- the slow timed passes of a 20-step run (gpurun trace,
     # profiles/bench_driver_cmd_r3.md)
+    def spin_up(fn) -> int:
+        """untimed passes of `fn` until `spinup` seconds have elapsed (the
+        clocks drop in the host-side gaps between measurements; every timed
+        figure starts from the same warm state); returns the steps run"""
+        if not (on_gpu and args.spinup > 0):
+            return 0
+        n = 0
+        t_end = time.perf_counter() + args.spinup
+        while True:
+            fn(args.tblock * 4)
+            sync()
+            n += args.tblock * 4
+            done = torch.tensor([1.0 if time.perf_counter() >= t_end else 0.0], device=dev)
+            comm.allreduce_(done, "min")
+            if done.item() >= 1.0:
+                return n
+
     spin = 0
     if on_gpu and args.spinup > 0:
         for k in range(1, args.tblock + 1):
             run(k)
             spin += k
-        t_end = time.perf_counter() + args.spinup
-        while True:
-            run(args.tblock * 4)
-            sync()
-            spin += args.tblock * 4
-            done = torch.tensor([1.0 if time.perf_counter() >= t_end else 0.0], device=dev)
-            comm.allreduce_(done, "min")
-            if done.item() >= 1.0:
-                break
+        spin += spin_up(run)
         for s in sim.subs.values():  # restart from the initial condition
             s.grid.buf.copy_(init_state[(s.blk.x0, s.blk.y0)])
             s.grid.iteration = 0
         sim.iteration = 0
 
-    def timed(k):
+    def timed(k, fn=None):
         """W warmup steps, then exactly k timed steps between barrier +
         synchronize; max over ranks (s). The native loop checks its in-kernel
         waits (and RCCL's asynchronous errors) at the end of every run and
         raises instead of reporting a number."""
-        run(args.warmup)
+        fn = fn or run
+        fn(args.warmup)
         barrier_sync()
         t0 = time.perf_counter()
-        run(k)
+        fn(k)
         sync()
         t1 = time.perf_counter()
         comm.barrier()
@@ -250,17 +260,16 @@ def main() -> int:
     # N > 1 points run, exchange off) on the same grid and the same uniform
     # initial field, so the N = 1 point of a scaling curve can be read
     # against the same schedule
+    # against the same schedule (same spin-up and warmup as the headline run:
+    # with 5 warmup steps right after the host-side gap the first passes ran
+    # at a lower clock, 0.166 vs 0.1315 ms/step in bench_dist_rank.py)
     secs_dist1 = None
     if on_gpu and comm.size == 1 and args.kernel == "pipe":
+        run_d = lambda k: sim.run_native(k, transport=2)  # noqa: E731
+        spin_up(run_d)
         for s in sim.subs.values():
             s.grid.buf.copy_(init_state[(s.blk.x0, s.blk.y0)])
-        run_d = lambda k: sim.run_native(k, transport=2)  # noqa: E731
-        run_d(args.warmup)
-        sync()
-        t0 = time.perf_counter()
-        run_d(args.steps)
-        sync()
-        secs_dist1 = time.perf_counter() - t0
+        secs_dist1 = timed(args.steps, run_d)
         sim.gate_check()
 
     # The same spin-up as the uniform run, on the random field (the power
@@ -277,15 +286,7 @@ def main() -> int:
             g, H = s.grid, s.grid.H
             g.buf[:, H:H + g.ny, H:H + g.nx] = torch.rand((g.ny, g.nx), generator=gen, device=dev) * 10.0
             rand_init[(s.blk.x0, s.blk.y0)] = g.buf.clone()
-        if args.spinup > 0:
-            t_end = time.perf_counter() + args.spinup
-            while True:
-                run(args.tblock * 4)
-                sync()
-                done = torch.tensor([1.0 if time.perf_counter() >= t_end else 0.0], device=dev)
-                comm.allreduce_(done, "min")
-                if done.item() >= 1.0:
-                    break
+        spin_up(run)
         for s in sim.subs.values():
             s.grid.buf.copy_(rand_init[(s.blk.x0, s.blk.y0)])
         sim.exchange(sim._cur()).wait()

@@ -24,12 +24,21 @@ def main() -> int:
     ap.add_argument("--algo", nargs="+", default=["radix", "merge", "torch"])
     ap.add_argument("--values", action="store_true", help="sort (key, 32-bit value) pairs")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--kind", default="random", choices=["random", "small", "sorted"],
+                    help="random: uniform 32-bit keys; small: keys < 2^16 (the high digits all zero); sorted")
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="tuning knobs name=value (cme213x.utils.tuning), e.g. radix_ds=10")
     a = ap.parse_args()
 
     import torch
 
     import cme213x  # noqa: F401
     from cme213x.ops.sort import sort
+    from cme213x.utils import tuning
+
+    knobs = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.tune}
+    for k, val in knobs.items():
+        tuning.set(k, val)
 
     dt = getattr(torch, a.dtype)
     for n in a.n:
@@ -39,7 +48,12 @@ def main() -> int:
         else:
             x = torch.randint(0, 2**31 - 1, (n,), device="cuda", dtype=torch.int64, generator=g)
             x = (x * 2 + (x & 1)).to(torch.int64) if dt == torch.uint32 else x - 2**30
+            if a.kind == "small":
+                x = x % 65536
             x = x.to(torch.int32).view(dt) if dt == torch.uint32 else x.to(dt)
+        if a.kind == "sorted":
+            x = torch.sort(x.to(torch.int64) if dt == torch.uint32 else x).values.to(x.dtype)
+            x = x.view(dt) if dt == torch.uint32 else x
         v = torch.arange(n, device="cuda", dtype=torch.int32) if a.values else None
         ref = torch.sort(x.to(torch.int64) if dt == torch.uint32 else x).values
         for algo in a.algo:
@@ -64,7 +78,8 @@ def main() -> int:
                 ts.append(e0.elapsed_time(e1))
             ts.sort()
             ms = ts[len(ts) // 2]
-            rec = {"bench": "sort", "algo": algo, "n": n, "dtype": a.dtype, "values": a.values, "ms": round(ms, 4),
+            rec = {"bench": "sort", "algo": algo, "n": n, "dtype": a.dtype, "values": a.values, "kind": a.kind,
+                   "tune": knobs, "ms": round(ms, 4),
                    "Gkeys_per_s": round(n / ms / 1e6, 2),
                    "eq_TBps_4pass": round(n * 4 * (2 if a.values else 1) * 2 * 4 / ms / 1e9, 2), "ok": ok}
             print(json.dumps(rec), flush=True)

@@ -89,7 +89,7 @@ const TuneEntry kTuneTable[cme::kTuneCount] = {
     {"CME_PIPE_VW", 0},          {"CME_PIPE_CHUNK", 0},         {"CME_PIPE_PER_CU", 0},
     {"CME_PIPE_THIN_MIN", 64},   {"CME_DIST_SCHEDULE", 2},      {"CME_DIST_EVENT_SCOPE", 0},
     {"CME_DIST_VERBOSE", 0},     {"CME_DIST_GATE_SPINS", 1L << 24}, {"CME_DIST_FAKE_XCHG_US", 0},
-    {"CME_RADIX_MAXBLOCKS", 1024}, {"CME_RADIX_DS", 2},          {"CME_STREAM2_CHUNK", 0},
+    {"CME_RADIX_MAXBLOCKS", 1024}, {"CME_RADIX_DS", 14},          {"CME_STREAM2_CHUNK", 0},
     {"CME_STREAMN_CHUNK", 0},    {"CME_STREAMN_ROUNDS", 0},     {"CME_STREAMN_MINCHUNK", 0},
     {"CME_STREAMN_THIN_WAVES", 1024}, {"CME_STREAMN_CAPPCT", 100}, {"CME_SPMVSCAN_MULTI", 1},
     {"CME_SPMV_NT", 1},          {"CME_SPMV_DIA1", 0},

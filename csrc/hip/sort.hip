@@ -10,9 +10,10 @@
 //                 counts[digit * nblocks + b]
 //   K2 scan     : one block per digit scans that digit's row of counts over
 //                 the blocks and writes the digit total (one small launch)
-//   K3 downsweep: block b re-reads its chunk tile by tile (4096 keys); keys are
-//                 ranked stably inside each wave with 8 ballots per item
-//                 (wave64 "match"), waves are combined per digit in LDS, the
+//   K3 downsweep: block b re-reads its chunk tile by tile (8192 keys); keys are
+//                 ranked stably inside each wave by one returning LDS atomic
+//                 per key (lanes resolve in lane order; ballot "match" on a
+//                 device that fails that check), waves are combined per digit in LDS, the
 //                 tile is reordered by digit in LDS and written out so that
 //                 consecutive lanes store consecutive addresses of a digit run.
 //                 A running per-digit base in LDS carries the chunk across tiles;
@@ -21,6 +22,8 @@
 // int32 / float32 keys are mapped to order-preserving uint32 codes by the
 // first pass's loads and back by the last pass's stores (no extra kernels).
 #include <stdlib.h>
+
+#include <atomic>
 
 #include "cme213/common.h"
 #include "cme213/tuning.h"
@@ -60,7 +63,20 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
     const bool vec = ((uintptr_t)keys & 15u) == 0;  // a tensor view may be 4-B aligned only
-    auto add = [&](uint32_t k) { atomicAdd(&hist[digit_of(rx_key_in(k, mode), shift)], 1u); };
+    // same-address lanes of one LDS atomic serialise (86 cycles per wave
+    // instruction when all 64 share a digit: the high digits of small keys),
+    // so a wave whose active lanes share one digit adds once
+    const int lane = lane_id();
+    auto add = [&](uint32_t k) {
+        const uint32_t d = digit_of(rx_key_in(k, mode), shift);
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+        if (__ballot(d != d0) == 0) {
+            const uint64_t act = __ballot(true);
+            if (lane == (int)__builtin_ctzll(act)) atomicAdd(&hist[d0], (uint32_t)__builtin_popcountll(act));
+        } else {
+            atomicAdd(&hist[d], 1u);
+        }
+    };
     // UNR 16-B loads in flight per lane before their LDS atomics (one load at
     // a time left the kernel waiting on HBM latency: wait-any 0.85 of its
     // cycles, profiles/sort_r3.md)
@@ -141,12 +157,28 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// ATOMIC_RANK: in-wave ranks through returning LDS atomics issued back to
-// back (else one LDS read-then-write per item); PREFETCH: the next tile's keys
-// load while this tile is reordered and stored (+16 VGPRs)
-// DS_THREADS: 256 (4096-key tiles) or 512 (8192-key tiles: digit runs of ~32
-// keys, i.e. fewer partially written lines per tile)
-template <bool HAS_VALUES, bool ATOMIC_RANK = false, bool PREFETCH = true, int DS_THREADS = kSortThreads>
+// In-wave rank kinds of the downsweep:
+//   kRankMatch  : ballot match (match_digit) + one LDS read-then-write per item
+//   kRankGroup  : ballot match + one returning LDS atomic per peer group
+//   kRankLanes  : one returning LDS atomic per LANE, no match. The lanes of a
+//                 wave-wide ds_add_rtn_u32 that hit one address are applied in
+//                 lane order (gfx950 LDS; benchmarks/probe_lds_atomic_order.hip:
+//                 1.29e9 lanes over 1-256 distinct digits and masked lanes, none
+//                 out of order), so lane l's old value counts the lower lanes of
+//                 its digit: a stable rank in one LDS instruction instead of ~40
+//                 VALU instructions per key. Same-address lanes serialise (86
+//                 cycles per wave-instruction at one digit, 6 at 256), so a wave
+//                 whose valid keys share one digit (the high digit of small
+//                 keys, sorted runs) takes one atomic for the whole group.
+//                 The library checks the lane order once per device before it
+//                 uses this kind (cme_radix_lane_order_probe) and falls back to
+//                 kRankMatch where the check fails.
+enum RadixRank { kRankMatch = 0, kRankGroup = 1, kRankLanes = 2 };
+
+// PREFETCH: the next tile's keys load while this tile is reordered and stored
+// (+16 VGPRs). DS_THREADS: 256 (4096-key tiles) or 512 (8192-key tiles: digit
+// runs of ~32 keys, i.e. fewer partially written lines per tile)
+template <bool HAS_VALUES, int RANK = kRankMatch, bool PREFETCH = true, int DS_THREADS = kSortThreads>
 __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_downsweep_kernel(
     const uint32_t* __restrict__ keys_in, uint32_t* __restrict__ keys_out, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ vals_out, long long n, long long chunk, int shift, int nblocks,
@@ -165,11 +197,41 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
     const int wid = threadIdx.x / kWave;
     const long long b0 = (long long)blockIdx.x * chunk;
     const long long b1 = b0 + chunk < n ? b0 + chunk : n;
+    __shared__ int s_identity;
     {  // digit bases: scan of the digit totals + this block's row prefix
         __shared__ uint32_t s_t[kWavesD];
         uint32_t tot;
-        const uint32_t db = block_exclusive_scan<kWavesD>(tid < kBins ? totals[tid] : 0u, s_t, tot, OpAdd());
+        const uint32_t td = tid < kBins ? totals[tid] : 0u;
+        if (tid == 0) s_identity = 0;
+        const uint32_t db = block_exclusive_scan<kWavesD>(td, s_t, tot, OpAdd());
         if (tid < kBins) s_base[tid] = db + prefix[(size_t)tid * nblocks + blockIdx.x];
+        if (tid < kBins && td == (uint32_t)n) s_identity = 1;  // every key has this digit
+        __syncthreads();
+    }
+    if (s_identity) {
+        // one digit holds every key: the stable pass is the identity
+        // permutation (the high digits of small keys) -- a straight copy,
+        // with the first / last pass's key transforms
+        constexpr int U = 8;
+        long long i = b0 + tid;
+        for (; i + (U - 1) * DS_THREADS < b1; i += U * DS_THREADS) {
+            uint32_t k[U], v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                k[u] = keys_in[i + u * DS_THREADS];
+                if constexpr (HAS_VALUES) v[u] = vals_in[i + u * DS_THREADS];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                keys_out[i + u * DS_THREADS] = rx_key_out(rx_key_in(k[u], mode_in), mode_out);
+                if constexpr (HAS_VALUES) vals_out[i + u * DS_THREADS] = v[u];
+            }
+        }
+        for (; i < b1; i += DS_THREADS) {
+            keys_out[i] = rx_key_out(rx_key_in(keys_in[i], mode_in), mode_out);
+            if constexpr (HAS_VALUES) vals_out[i] = vals_in[i];
+        }
+        return;
     }
 
     // warp-striped: item k of lane l = key t0 + wid*1024 + k*64 + l (memory order = (k, l));
@@ -201,7 +263,31 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
 #pragma unroll
             for (int k = 0; k < kItems; ++k) key[k] = rx_key_in(key[k], mode_in);
         }
-        if constexpr (!ATOMIC_RANK) {
+        if constexpr (RANK == kRankLanes) {
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const bool ok = k < nk;
+                const uint32_t d = digit_of(key[k], shift);
+                const uint64_t act = __ballot(ok);
+                if (act == 0) {
+                    rank[k] = 0xffffffffu;
+                    continue;
+                }
+                const int first = (int)__builtin_ctzll(act);
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+                if (__ballot(ok && d != d0) == 0) {  // one digit: one atomic, ranks by lane count
+                    uint32_t base = 0;
+                    if (lane == first) base = atomicAdd(&s_whist[wid][d0], (uint32_t)__builtin_popcountll(act));
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
+                    const uint32_t below = (uint32_t)__builtin_popcountll(act & ((1ull << lane) - 1ull));
+                    rank[k] = ok ? base + below : 0xffffffffu;
+                } else {
+                    uint32_t old = 0xffffffffu;
+                    if (ok) old = atomicAdd(&s_whist[wid][d], 1u);
+                    rank[k] = old;
+                }
+            }
+        } else if constexpr (RANK == kRankMatch) {
 #pragma unroll
             for (int k = 0; k < kItems; ++k) {
                 const bool ok = k < nk;
@@ -262,6 +348,9 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
             if (tid < kBins) {
                 s_tile_off[tid] = ex;
                 s_gdiff[tid] = s_base[tid] - ex;
+                // fold the tile offset into every wave's prefix: one LDS read per key below
+#pragma unroll
+                for (int w = 0; w < kWavesD; ++w) s_whist[w][tid] += ex;
             }
         }
         __syncthreads();
@@ -270,7 +359,7 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
         for (int k = 0; k < kItems; ++k) {
             if (rank[k] != 0xffffffffu) {
                 const uint32_t d = digit_of(key[k], shift);
-                const uint32_t pos = s_tile_off[d] + s_whist[wid][d] + rank[k];
+                const uint32_t pos = s_whist[wid][d] + rank[k];
                 s_keys[pos] = key[k];
                 if constexpr (HAS_VALUES) s_vals[pos] = val[k];
             }
@@ -549,12 +638,83 @@ CME_EXPORT long long cme_radix_ws_bytes(long long n) {
 // [bit0, bit1), ping-ponging through `tmp` so that the last pass writes out;
 // values (optional) likewise. mode: 0 uint32, 1 int32, 2 float32 keys.
 // ws: cme_radix_ws_bytes(n) bytes.
-// downsweep variant (CME_RADIX_DS, for A/B sweeps): bit 0 atomic ranks, bit 1
-// prefetch, bit 2 8192-key tiles (512 threads). Default 2: the four arms are within 3 % of each other at 16M keys
-// (0.348-0.357 ms; the ranking's LDS round trips are not what binds), the
-// prefetch without atomic ranks is best at 48M (0.956 vs 0.981 ms;
-// profiles/sort_r3.md)
-static int radix_ds_variant() { return (int)(cme::tune_get(cme::kTuneRadixDS) & 7); }
+// downsweep variant (CME_RADIX_DS, for A/B sweeps): bit 0 group-atomic ranks,
+// bit 1 prefetch, bit 2 8192-key tiles (512 threads), bit 3 lane-order atomic
+// ranks (kRankLanes; overrides bit 0). Default 14 = lane ranks + prefetch +
+// 8192-key tiles (profiles/sort_r4.md, one box: 16M uint32 0.218 ms vs 0.265
+// for the round-3 default 2 = ballot-match ranks + prefetch; 48M 0.684 vs
+// 0.821; 16M int32 key-value 0.378 vs 0.440). With the match gone the larger
+// tiles win (digit runs of ~32 keys: fewer partial lines written), where they
+// lost to the barrier rounds before.
+static int radix_ds_variant() { return (int)(cme::tune_get(cme::kTuneRadixDS) & 15); }
+
+namespace {
+// Lane-order check for kRankLanes: one block; every wave runs `trials`
+// wave-wide returning atomics over digit patterns of 1..256 distinct values
+// with masked lanes, and counts the lanes whose old value is not (running
+// count + lower active lanes of the digit). Vector atomics only.
+__global__ __launch_bounds__(256) void radix_lane_order_probe_kernel(int trials, unsigned* __restrict__ bad) {
+    __shared__ uint32_t cnt[4][kBins];
+    const int lane = lane_id(), w = threadIdx.x / kWave;
+    for (int i = threadIdx.x; i < 4 * kBins; i += 256) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    unsigned nbad = 0;
+    for (int t = 0; t < trials; ++t) {
+        uint32_t h = (uint32_t)(t * 4 + w) * 0x9e3779b9u + (uint32_t)lane * 0x85ebca6bu;
+        h ^= h >> 15;
+        h *= 0x2c1b3c6du;
+        h ^= h >> 12;
+        const int ndist = 1 << (t % 9);  // 1 .. 256 distinct digits
+        const uint32_t d = (h >> 8) % (uint32_t)ndist;
+        const bool on = (h & 15u) != 0u;  // ~6 % masked lanes
+        const uint32_t before = cnt[w][d];
+        uint32_t lower = 0;
+        for (int l = 0; l < kWave; ++l) {
+            const uint32_t dl = (uint32_t)__shfl((int)d, l);
+            const int onl = __shfl((int)on, l);
+            lower += (l < lane && onl && dl == d) ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t old = 0;
+        if (on) old = atomicAdd(&cnt[w][d], 1u);
+        __builtin_amdgcn_wave_barrier();
+        nbad += (on && old != before + lower) ? 1u : 0u;
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+std::atomic<int> g_lane_order[64];  // per device: 0 unknown, 1 lane-ordered, -1 not (or not checkable)
+}  // namespace
+
+// 1 if the device's returning LDS atomics resolve same-address lanes in lane
+// order (kRankLanes is then used), 0 if not. Runs the check once per device
+// (~1 ms, synchronous on a private stream); under stream capture
+// an unchecked device reports 0 without checking.
+CME_EXPORT int cme_radix_lane_order(int check) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    const int st = g_lane_order[dev].load();
+    if (st != 0 || !check) return st > 0;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 0;
+    unsigned* bad = nullptr;
+    int ok = -1;
+    if (hipMallocAsync((void**)&bad, 4, s) == hipSuccess) {
+        unsigned hb = 1;
+        if (hipMemsetAsync(bad, 0, 4, s) == hipSuccess) {
+            hipLaunchKernelGGL(radix_lane_order_probe_kernel, dim3(1), dim3(256), 0, s, 9 * 48, bad);
+            if (hipGetLastError() == hipSuccess &&
+                hipMemcpyAsync(&hb, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                hipStreamSynchronize(s) == hipSuccess)
+                ok = hb == 0 ? 1 : -1;
+        }
+        (void)hipFreeAsync(bad, s);
+        (void)hipStreamSynchronize(s);
+    }
+    (void)hipStreamDestroy(s);
+    g_lane_order[dev].store(ok);
+    return ok > 0;
+}
 
 CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
                               uint32_t* vtmp, long long n, int mode, int bit0, int bit1, void* ws, void* stream) {
@@ -563,7 +723,13 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     if (bit0 < 0 || bit1 > 32 || bit1 <= bit0 || mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) ||
         (vin && !vtmp) || n >= (1ll << 32))
         return (int)hipErrorInvalidValue;
-    const int dsv = radix_ds_variant();
+    int dsv = radix_ds_variant();
+    if (dsv & 8) {  // lane-order ranks: only on a device that passed the check
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+        if (!cme_radix_lane_order(capturing ? 0 : 1)) dsv &= ~8;
+    }
+    const bool lanes = (dsv & 8) != 0;
     const bool wide = (dsv & 4) != 0;  // 8192-key downsweep tiles
     const long long dtile = wide ? 2 * kSortTile : kSortTile;
     const long long tiles = (n + dtile - 1) / dtile;
@@ -594,16 +760,24 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
             hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P>), dim3(nb), dim3(kSortThreads), 0, s, ki, ko, vi,  \
                                vo, n, chunk, shift, nb, counts, totals, mi, mo);                                  \
     } while (0)
+        // arms: 0-3 ballot-match ranks (bit 0 group atomics, bit 1 prefetch),
+        // 4-5 lane ranks (without / with prefetch); `wide` picks the 512-thread
+        // 8192-key tile instantiation of any arm
+        const int arm = lanes ? 4 + ((dsv >> 1) & 1) : (dsv & 3);
         if (vin) {
-            if (dsv == 0) CME_DS(true, false, false);
-            else if (dsv == 1) CME_DS(true, true, false);
-            else if (dsv == 2) CME_DS(true, false, true);
-            else CME_DS(true, true, true);
+            if (arm == 0) CME_DS(true, kRankMatch, false);
+            else if (arm == 1) CME_DS(true, kRankGroup, false);
+            else if (arm == 2) CME_DS(true, kRankMatch, true);
+            else if (arm == 3) CME_DS(true, kRankGroup, true);
+            else if (arm == 4) CME_DS(true, kRankLanes, false);
+            else CME_DS(true, kRankLanes, true);
         } else {
-            if (dsv == 0) CME_DS(false, false, false);
-            else if (dsv == 1) CME_DS(false, true, false);
-            else if (dsv == 2) CME_DS(false, false, true);
-            else CME_DS(false, true, true);
+            if (arm == 0) CME_DS(false, kRankMatch, false);
+            else if (arm == 1) CME_DS(false, kRankGroup, false);
+            else if (arm == 2) CME_DS(false, kRankMatch, true);
+            else if (arm == 3) CME_DS(false, kRankGroup, true);
+            else if (arm == 4) CME_DS(false, kRankLanes, false);
+            else CME_DS(false, kRankLanes, true);
         }
 #undef CME_DS
         CME_TRY(hipGetLastError());

@@ -172,7 +172,7 @@ def test_merge_sort_skewed_and_stable(gpu, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arm", [0, 1, 3, 4, 5, 7])
+@pytest.mark.parametrize("arm", [0, 1, 2, 3, 4, 5, 7, 8, 10, 14])
 def test_radix_downsweep_arms(gpu, arm):
     """Every reduce-then-scan downsweep arm (tuning knob radix_ds: atomic
     ranks, next-tile prefetch, 8192-key tiles) sorts keys and key-value pairs
@@ -193,3 +193,40 @@ def test_radix_downsweep_arms(gpu, arm):
             assert torch.equal(vs.cpu().long(), ri), n
             assert torch.equal(sort(k, algo="radix").cpu().long(), rk), n
     assert not tuning.is_set("radix_ds")  # restored to the environment default
+
+
+@pytest.mark.gpu
+def test_radix_lane_order_probe(gpu):
+    """The device passes the lane-order check the lane-atomic ranks rely on
+    (benchmarks/probe_lds_atomic_order.hip measured it on gfx950), and the
+    answer is cached per device."""
+    from cme213x.ops.sort import radix_lane_order
+
+    assert radix_lane_order(check=True)
+    assert radix_lane_order(check=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arm", [2, 10, 14])
+@pytest.mark.parametrize("kind", ["equal", "sorted", "reversed", "fewbits", "small", "twovals"])
+def test_radix_lane_ranks_low_entropy_stable(gpu, arm, kind):
+    """Lane-atomic ranks (arm 10) against the ballot-match arm (2) and a
+    stable CPU sort on inputs whose waves see one or a few digits: all keys
+    equal, sorted / reversed runs, few bits, small keys (high digits all
+    zero: the one-atomic-per-wave path), two values interleaved."""
+    from cme213x.ops.sort import sort
+    from cme213x.utils import tuning
+
+    n = 3 * (1 << 20) + 1234
+    if kind == "small":
+        k = torch.randint(0, 1 << 12, (n,), dtype=torch.int32)
+    elif kind == "twovals":
+        k = (torch.arange(n, dtype=torch.int32) % 2) * 0x01010101
+    else:
+        k = _keys(n, torch.int32, kind)
+    v = torch.arange(n, dtype=torch.int32)
+    with tuning.override(radix_ds=arm):
+        ks, vs = sort(k.to(gpu), values=v.to(gpu), algo="radix")
+    ref = torch.sort(k.long(), stable=True)
+    assert torch.equal(ks.cpu().long(), ref.values)
+    assert torch.equal(vs.cpu().long(), ref.indices)
