@@ -367,13 +367,21 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
         __syncthreads();
         if (PREFETCH && t0 + kTileD < b1) load_tile(t0 + kTileD);  // in flight during the stores
         const int tile_n = (int)((b1 - t0) < kTileD ? (b1 - t0) : kTileD);
-        for (int i = threadIdx.x; i < tile_n; i += DS_THREADS) {
-            const uint32_t k = s_keys[i];
-            const uint32_t d = digit_of(k, shift);
-            const uint32_t g = s_gdiff[d] + (uint32_t)i;
-            keys_out[g] = rx_key_out(k, mode_out);
-            if constexpr (HAS_VALUES) vals_out[g] = s_vals[i];
-        }
+        // the key transform only on the last pass (a uniform branch: the
+        // branch-free select chain cost ~5 VALU per key on every pass)
+        auto store_tile = [&](int mo) {
+            for (int i = threadIdx.x; i < tile_n; i += DS_THREADS) {
+                const uint32_t k = s_keys[i];
+                const uint32_t d = digit_of(k, shift);
+                const uint32_t g = s_gdiff[d] + (uint32_t)i;
+                keys_out[g] = mo ? rx_key_out(k, mo) : k;
+                if constexpr (HAS_VALUES) vals_out[g] = s_vals[i];
+            }
+        };
+        if (mode_out == 0)
+            store_tile(0);
+        else
+            store_tile(mode_out);
         __syncthreads();
         // advance the per-digit bases by this tile's counts
         if (tid < kBins) {
