@@ -34,7 +34,7 @@ import time
 import numpy as np
 import torch
 
-from ..ops.stencil import heat_run, heat_step, heat_stepn
+from ..ops.stencil import arith_code, heat_run, heat_step, heat_stepn
 from ..parallel.comm import Comm, LoopbackComm, P2P, Pending
 from ..parallel.decomp import Block, decompose
 from ..utils.params import SimParams
@@ -274,11 +274,17 @@ class DistHeat:
             raise ValueError("kernel='tile' runs single-grid (world 1, non-periodic) passes only")
         if tblock > 3 and dtype == torch.float64 and kernel == "streamn" and torch.device(device).type == "cuda":
             raise ValueError("fp64 4-step passes need kernel='pipe' on the GPU (streamN fp64 stops at 3)")
-        self.fma = bool(fma)
+        # arithmetic: 0 exact, 1 FMA-contracted, 2 reassociated ("fast": fma="fast";
+        # fp32 order 8, the pipelined kernel for multi-step passes on the GPU)
+        self.arith = arith_code(fma)
+        if self.arith == 2 and tblock > 1 and (dtype != torch.float32 or params.order != 8 or kernel == "tile"
+                                               or (kernel != "pipe" and torch.device(device).type == "cuda")):
+            raise ValueError("fma='fast' multi-step passes: fp32, order 8, kernel='pipe'")
+        self.fma = self.arith == 1
         # 3-4 step passes: streamN (one wave holds every step) or the
         # wave-pipelined kernel (csrc/hip/heat_pipe.hip); identical results
         self.kernel = kernel
-        self.variant = "fma" if self.fma else variant
+        self.variant = {1: "fma", 2: "fast"}.get(self.arith, variant)
         self.tblock = tblock
         self.device = torch.device(device)
         self.subs: dict[int, _Sub] = {}
@@ -293,8 +299,12 @@ class DistHeat:
 
     def _flags(self) -> int:
         """Kernel flags of the native loop (cme_heat_dist_run): bit 0 FMA,
-        bit 1 the pipelined NS-step kernel."""
-        return int(self.fma) | (2 if self.kernel == "pipe" else 0)
+        bit 1 the pipelined NS-step kernel, bit 3 reassociated arithmetic."""
+        return int(self.fma) | (2 if self.kernel == "pipe" else 0) | (8 if self.arith == 2 else 0)
+
+    def _fma_arg(self):
+        """the ``fma`` argument of the stencil ops for this solver's arithmetic"""
+        return "fast" if self.arith == 2 else self.fma
 
     def _cur(self) -> int:
         return next(iter(self.subs.values())).grid.cur
@@ -413,7 +423,7 @@ class DistHeat:
                 regs = list(regions_of(s, self.tblock * g.B))
                 if regs:
                     heat_stepn(g.buf[k], g.buf[1 - k], regs, _ext_region(s), g.order, g.xcfl, g.ycfl, ns,
-                               fma=self.fma, kernel=self.kernel)
+                               fma=self._fma_arg(), kernel=self.kernel)
 
         if sync:
             sweep(_interior_regions)
@@ -664,6 +674,8 @@ class DistHeat:
         steps per HBM pass on the chosen pass kernel, FMA or exact."""
         if self.tblock == 1:
             return self.variant
+        if self.arith == 2:
+            return f"pipe{self.tblock}_fast"
         suffix = "_fma" if self.fma else ""
         if self.kernel == "tile":
             return f"tile{self.tblock}" + suffix
@@ -929,7 +941,7 @@ def native_selftest(sim: "DistHeat", kind: str, handle, fused: bool, n: int = 10
     p = SimParams(nx=min(p0.nx, n), ny=min(p0.ny, n), iters=iters, order=p0.order, ic=5.0,
                   bc=(0.0, 10.0, 3.0, 7.0), grid_method=p0.grid_method, sync=p0.sync, flavor="hw5")
     dt = next(iter(sim.subs.values())).grid.dtype
-    kw = dict(local_ranks=list(sim.local_ranks), world=sim.world, periodic=sim.periodic, fma=sim.fma)
+    kw = dict(local_ranks=list(sim.local_ranks), world=sim.world, periodic=sim.periodic, fma=sim._fma_arg())
     a = DistHeat(p, sim.comm, dt, sim.device, tblock=sim.tblock, kernel=sim.kernel, **kw)
     b = DistHeat(p, sim.comm, dt, sim.device, tblock=1, **kw)
     for d in (a, b):

@@ -33,6 +33,10 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_gate_status", "p")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_gated_f32", "ppiipipiiffiipupp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_gated_f64", "ppiipipiiddiipupp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_info", "pp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f32", "ppiiiiiiiffp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f64", "ppiiiiiiiddp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_fast_f32", "ppiipipiiffiipupp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_run_fast_f32", "ppiiiiiiiiffipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -63,6 +67,25 @@ FP32_ONLY = {"stream4", "stream4_fma", "pipe5", "pipe5_fma", "pipe6", "pipe6_fma
 # std::fma oracle, every other variant name the exact (contraction-off) one
 FMA_VARIANTS = {"stream2_fma", "stream_fma", "fma", "stream3_fma", "stream4_fma", "pipe3_fma", "pipe4_fma",
                 "pipe5_fma", "pipe6_fma", "tile1_fma", "tile2_fma", "tile3_fma", "tile4_fma"}
+# reassociated ("fast") arithmetic (csrc/hip/heat_fast.hip; CPU: the fast
+# oracle): name -> timesteps per pass. "fast" is a single step (any order,
+# fp32 / fp64); pipeN_fast are wide-lane pipelined passes, fp32 order 8
+FAST_VARIANTS = {"fast": 1, "pipe2_fast": 2, "pipe3_fast": 3, "pipe4_fast": 4}
+
+
+def arith_code(fma) -> int:
+    """Arithmetic of a pass: False / 0 exact, True / 1 FMA-contracted,
+    "fast" / 2 reassociated (the flags word of the native entry points)."""
+    if fma == "fast" or (not isinstance(fma, bool) and fma == 2):
+        return 2
+    if fma in (True, False, 0, 1, "fma", "exact"):
+        return 1 if fma in (True, 1, "fma") else 0
+    raise ValueError(f"arithmetic must be exact / fma / fast, got {fma!r}")
+
+
+def _check_fast(t: torch.Tensor, order: int, nsteps: int) -> None:
+    if nsteps > 1 and (t.dtype != torch.float32 or order != 8):
+        raise ValueError("reassociated multi-step passes: fp32, order 8")
 
 
 def _check(prev: torch.Tensor, curr: torch.Tensor) -> None:
@@ -82,11 +105,19 @@ def heat_step(prev: torch.Tensor, curr: torch.Tensor, region: tuple[int, int, in
               xcfl: float, ycfl: float, variant: str = "stream", chunk: int = 0) -> None:
     """curr[region] = FTCS(prev); region = (xb, xe, yb, ye) in grid coords."""
     _check(prev, curr)
-    if variant in MULTISTEP or variant in TILE_VARIANTS:
+    if variant in MULTISTEP or variant in TILE_VARIANTS or FAST_VARIANTS.get(variant, 1) > 1:
         raise ValueError(f"variant {variant!r} is a multi-step / whole-interior pass; use heat_run")
     xb, xe, yb, ye = map(int, region)
     rows, pitch = prev.shape
     f64 = prev.dtype == torch.float64
+    if variant == "fast":
+        if prev.is_cuda:
+            _ext.call_hip("cme_heat_step_fast_f64" if f64 else "cme_heat_step_fast_f32", prev.data_ptr(),
+                          curr.data_ptr(), pitch, rows, xb, xe, yb, ye, order, xcfl, ycfl, _ext.stream_ptr(prev.device))
+        else:
+            _ext.call_cpu("cme_cpu_heat_step_fast_f64" if f64 else "cme_cpu_heat_step_fast_f32", prev.data_ptr(),
+                          curr.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl)
+        return
     if prev.is_cuda:
         name = "cme_heat_step_f64" if f64 else "cme_heat_step_f32"
         _ext.call_hip(name, prev.data_ptr(), curr.data_ptr(), pitch, rows, xb, xe, yb, ye, order,
@@ -131,6 +162,8 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
     Bitwise equal to ``nsteps`` single steps; fp64 4-step passes need
     ``kernel="pipe"``. ``kernel="pipe"`` (3 or 4 steps) runs the wave-pipelined pass
     (csrc/hip/heat_pipe.hip) instead of streamN: same cells, same bits.
+    ``fma``: False exact, True FMA-contracted, "fast" reassociated (fp32
+    order 8 for nsteps > 1: the wide-lane pipelined pass of heat_fast.hip).
     On CPU it runs exactly those single steps through temporaries."""
     if kernel not in ("streamn", "pipe"):
         raise ValueError("kernel must be 'streamn' or 'pipe'")
@@ -139,14 +172,18 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
         regions = [regions]
     if not 1 <= len(regions) <= 4:
         raise ValueError("1 to 4 output regions per pass")
+    arith = arith_code(fma)
+    single = ("naive", "fma", "fast")[arith] if not prev.is_cuda else ("stream", "fma", "fast")[arith]
     if nsteps == 1:
         for reg in regions:
-            heat_step(prev, curr, reg, order, xcfl, ycfl, "fma" if fma else ("stream" if prev.is_cuda else "naive"))
+            heat_step(prev, curr, reg, order, xcfl, ycfl, single)
         return
     if not 2 <= nsteps <= 4:
         raise ValueError("nsteps must be 1..4")
+    if arith == 2:
+        _check_fast(prev, order, nsteps)
     if not prev.is_cuda:
-        v = "fma" if fma else "naive"
+        v = ("naive", "fma", "fast")[arith]
         src = prev
         for _ in range(nsteps - 1):
             tmp = prev.clone()
@@ -162,6 +199,11 @@ def heat_stepn(prev: torch.Tensor, curr: torch.Tensor, regions, ext: tuple[int, 
     flat = [int(v) for reg in regions for v in reg]
     r = (ctypes.c_int * len(flat))(*flat)
     e = (ctypes.c_int * 4)(*map(int, ext))
+    if arith == 2:
+        _ext.call_hip("cme_heat_pipe_fast_f32", prev.data_ptr(), curr.data_ptr(), pitch, rows, ctypes.addressof(r),
+                      len(regions), ctypes.addressof(e), order, nsteps, xcfl, ycfl, chunk, 0, None, 0, None,
+                      _ext.stream_ptr(prev.device))
+        return
     name = "cme_heat_stepn_f64" if f64 else "cme_heat_stepn_f32"
     if kernel == "pipe" and nsteps >= 3:
         name = "cme_heat_pipe_f64" if f64 else "cme_heat_pipe_f32"
@@ -197,6 +239,18 @@ def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int]
     f64 = a.dtype == torch.float64
     if f64 and variant in FP32_ONLY:
         raise ValueError(f"variant {variant!r} is fp32 only")
+    if variant in FAST_VARIANTS:
+        ns = FAST_VARIANTS[variant]
+        if a.is_cuda and ns > 1:
+            _check_fast(a, order, ns)
+            final = ctypes.c_int(0)
+            _ext.call_hip("cme_heat_run_fast_f32", a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, ns,
+                          xcfl, ycfl, iters, ctypes.addressof(final), _ext.stream_ptr(a.device))
+            return b if final.value else a
+        for i in range(iters):  # single steps (every pass length gives the same bits)
+            src, dst = (a, b) if i % 2 == 0 else (b, a)
+            heat_step(src, dst, region, order, xcfl, ycfl, "fast")
+        return a if iters % 2 == 0 else b
     if a.is_cuda:
         name = "cme_heat_run_f64" if f64 else "cme_heat_run_f32"
         final = ctypes.c_int(0)

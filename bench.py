@@ -39,7 +39,7 @@ def selftest(comm, dev, args) -> bool:
     """Bitwise self-test of the N = 1 timed path (the native multi-pass
     driver, ``heat_run``): a 1024^2 problem with a non-uniform interior runs
     2*tblock+1 timesteps (whole passes plus a tail) and must equal, bit for
-    bit, the same number of single FMA steps. (N > 1: the solver's own
+    bit, the same number of single steps of the same arithmetic. (N > 1: the solver's own
     :meth:`DistHeat.enable_native` self-test of the native loop against the
     torch.distributed loop.)"""
     import torch
@@ -50,9 +50,9 @@ def selftest(comm, dev, args) -> bool:
     iters = 2 * args.tblock + 1
     p = SimParams(nx=1024, ny=1024, iters=iters, order=args.order, ic=5.0, bc=(0.0, 10.0, 3.0, 7.0),
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
-    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=bool(args.fma),
+    a = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock, fma=args.fma_arg,
                  kernel=args.kernel)
-    b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1, fma=bool(args.fma))
+    b = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=1, fma=args.fma_arg)
     # non-uniform interior so a misplaced pass boundary changes the answer
     for sim in (a, b):
         s = next(iter(sim.subs.values()))
@@ -99,9 +99,14 @@ def main() -> int:
     ap.add_argument("--method", type=int, default=1, help="1 = 1-D stripes, 2 = 2-D blocks")
     ap.add_argument("--mode", choices=["async", "sync"], default="async")
     ap.add_argument("--variant", default="stream")
-    ap.add_argument("--fma", type=int, choices=[0, 1], default=1,
-                    help="FMA-contracted stencil (what nvcc emits for the reference's GPU kernels); 0 = exact "
-                         "contraction-off arithmetic, bitwise equal to the non-FMA CPU oracle")
+    ap.add_argument("--fma", type=int, choices=[0, 1], default=None,
+                    help="1 = --arith fma, 0 = --arith exact")
+    ap.add_argument("--arith", choices=["fma", "exact", "fast"], default=None,
+                    help="stencil arithmetic (default fast): fma = FMA-contracted (what nvcc emits for the "
+                         "reference's GPU kernel), exact = no contraction (bitwise = the CPU oracle), fast = "
+                         "reassociated (CFL folded into the weights, symmetric pairs summed first: 17 instead of "
+                         "20 flop-instructions per point; within the reference's 10-ULP criterion of exact, "
+                         "bitwise = the CPU fast oracle); profiles/heat_fast_r4.md has the A/B on one box")
     ap.add_argument("--tblock", type=int, choices=[0, 1, 2, 3, 4], default=0,
                     help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos); "
                          "0 = by subdomain size (auto_tblock)")
@@ -129,6 +134,11 @@ def main() -> int:
     args = ap.parse_args()
     if args.share_gpu:
         args.transport = "ipc"
+    if args.arith is None:
+        args.arith = "fast" if args.fma is None else ("fma" if args.fma else "exact")
+    args.fma = int(args.arith == "fma")
+    # the solver's `fma` argument: False exact, True FMA-contracted, "fast" reassociated
+    args.fma_arg = {"exact": False, "fma": True, "fast": "fast"}[args.arith]
 
     import torch
     import torch.distributed as dist
@@ -159,7 +169,7 @@ def main() -> int:
                   grid_method=args.method, sync=(args.mode == "sync"), flavor="hw5")
 
     sim = DistHeat(p, comm, torch.float32, dev, variant=args.variant if on_gpu else "naive", tblock=args.tblock,
-                   fma=bool(args.fma), kernel=args.kernel,
+                   fma=args.fma_arg, kernel=args.kernel,
                    native=("off" if (not on_gpu or comm.size == 1) else args.native))
     # N > 1: the solver's own native-loop setup -- transport, then a bitwise
     # self-test against the torch.distributed loop (fused schedule first,
@@ -252,14 +262,9 @@ def main() -> int:
     secs = timed(args.steps)
     sanity_ok = sane()
 
-    # the same K steps from a random-init field (BASELINE.json: "synthetic
-    # random-init inputs"): uniform(0, 10) interior, seeded per rank, same
-    # BCs. The pass is issue/power bound, and random data toggles more bits
-    # than the reference's uniform IC, so this is the slower figure.
     # N = 1: the distributed native schedule (cme_heat_dist_run, the loop the
     # N > 1 points run, exchange off) on the same grid and the same uniform
     # initial field, so the N = 1 point of a scaling curve can be read
-    # against the same schedule
     # against the same schedule (same spin-up and warmup as the headline run:
     # with 5 warmup steps right after the host-side gap the first passes ran
     # at a lower clock, 0.166 vs 0.1315 ms/step in bench_dist_rank.py)
@@ -272,6 +277,10 @@ def main() -> int:
         secs_dist1 = timed(args.steps, run_d)
         sim.gate_check()
 
+    # the same K steps from a random-init field (BASELINE.json: "synthetic
+    # random-init inputs"): uniform(0, 10) interior, seeded per rank, same
+    # BCs. The pass is issue/power bound, and random data toggles more bits
+    # than the reference's uniform IC, so this is the slower figure.
     # The same spin-up as the uniform run, on the random field (the power
     # controller settles to the data's switching activity over ~10 ms: a
     # 20-step window right after the switch from the uniform field ran 0.20
@@ -330,12 +339,14 @@ def main() -> int:
                 "parallelism": f"{'stripes' if args.method == 1 else 'blocks'}{args.gpus}-{args.mode}",
                 "variant": (args.variant if args.tblock == 1 else
                             f"{'pipe' if args.kernel == 'pipe' and args.tblock >= 3 else 'stream'}{args.tblock} "
-                            f"({args.tblock} steps/pass)") + (" fma" if args.fma else " exact"),
+                            f"({args.tblock} steps/pass)") + f" {args.arith}",
                 "kernel": args.kernel,
                 # pipelined fp32 pass: 8 columns per lane at order 8 (tuning knob pipe_vw = 4 / 8 forces one width)
                 "lane_columns": ({4: 4, 8: 8}.get(pipe_vw, 8 if args.order == 8 else 4)
                                  if args.kernel == "pipe" and args.tblock >= 3 else 4),
                 "fma": bool(args.fma),
+                "arith": {"fma": "FMA-contracted", "exact": "exact (no contraction)",
+                          "fast": "reassociated (folded CFL weights, pair sums; <= 10 ULP of exact)"}[args.arith],
                 "tblock": args.tblock,
                 "device": args.device,
                 "rehearsal_shared_gpu": bool(args.share_gpu),

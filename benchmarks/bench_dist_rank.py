@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--method", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--fma", type=int, default=1)
+    ap.add_argument("--arith", choices=["fma", "exact", "fast"], default=None,
+                    help="stencil arithmetic (overrides --fma); fast = reassociated (csrc/hip/heat_fast.hip)")
     ap.add_argument("--tblock", type=int, default=3, help="timesteps per exchange / HBM pass (1-4)")
     ap.add_argument("--native", type=int, default=1, help="1: native loop (null transport); 0: Python loop")
     ap.add_argument("--reps", type=int, default=5)
@@ -62,7 +64,9 @@ def main():
     for w in args.world:
         rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
         p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=False, flavor="hw5")
-        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=bool(args.fma),
+        arith = args.arith or ("fma" if args.fma else "exact")
+        fma_arg = {"exact": False, "fma": True, "fast": "fast"}[arith]
+        sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=fma_arg,
                       kernel=args.kernel)
 
         def run(k):
@@ -84,6 +88,7 @@ def main():
         ms = sorted(times)[len(times) // 2]
         base = base or ms * w
         print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
+                          "arith": arith,
                           "kernel": args.kernel, "tune": knobs,
                           "reps": args.reps,
                           "ms_per_step": round(ms, 4),

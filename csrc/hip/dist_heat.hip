@@ -64,6 +64,13 @@ extern "C" int cme_heat_pipe_gated_f64(const double* prev, double* curr, int pit
 extern "C" int cme_heat_stepn_f64(const double* prev, double* curr, int pitch, int gy, const int* out, int nout,
                                   const int* ext, int order, int nsteps, double xcfl, double ycfl, int chunk, int fma,
                                   void* stream);
+// heat_fast.hip: reassociated arithmetic (fp32, order 8 for the passes)
+extern "C" int cme_heat_step_fast_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb,
+                                      int ye, int order, float xcfl, float ycfl, void* stream);
+extern "C" int cme_heat_pipe_fast_f32(const float* prev, float* curr, int pitch, int gy, const int* out, int nout,
+                                      const int* ext, int order, int nsteps, float xcfl, float ycfl, int chunk,
+                                      int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
+                                      void* stream);
 
 #define CME_TRY_INT(expr)                 \
     do {                                  \
@@ -395,7 +402,13 @@ int launch_wait(const FlagList& l, unsigned v, unsigned* timeout, hipStream_t s)
     return 0;
 }
 
-// single step: streaming kernel, exact (variant 2) or FMA (variant 6)
+// bit 3 of the flags word: reassociated ("fast") arithmetic, fp32 order 8
+// (heat_fast.hip: the wide-lane pipelined pass with FMA arm 5 for 2-4 step
+// passes, a plain kernel for single steps)
+constexpr int kArithFast = 8;
+
+// single step: streaming kernel, exact (variant 2) or FMA (variant 6), or the
+// reassociated kernel
 template <typename T>
 int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T xcfl, T ycfl, int fma,
                 hipStream_t s);
@@ -403,6 +416,8 @@ int step_region(const T* p, T* c, int pitch, int gy, const int* r, int order, T 
 template <>
 int step_region<float>(const float* p, float* c, int pitch, int gy, const int* r, int order, float xcfl, float ycfl,
                        int fma, hipStream_t s) {
+    if (fma & kArithFast)
+        return cme_heat_step_fast_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, xcfl, ycfl, (void*)s);
     return cme_heat_step_f32(p, c, pitch, gy, r[0], r[1], r[2], r[3], order, (fma & 1) ? 6 : 2, xcfl, ycfl, 0,
                              (void*)s);
 }
@@ -427,6 +442,9 @@ int stepn_regions(const T* p, T* c, int pitch, int gy, const int* r, int n, cons
 template <>
 int stepn_regions<float>(const float* p, float* c, int pitch, int gy, const int* r, int n, const int* ext, int order,
                          int ns, float xcfl, float ycfl, int fma, hipStream_t s) {
+    if (fma & kArithFast)
+        return cme_heat_pipe_fast_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, 0, nullptr, 0u, nullptr,
+                                      (void*)s);
     if ((fma & kKernelPipe) && ns >= 3)
         return cme_heat_pipe_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
     return cme_heat_stepn_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, fma & 1, (void*)s);
@@ -445,9 +463,13 @@ template <typename T>
 int gated_pass(const T* p, T* c, int pitch, int gy, const int* r, int n, const int* ext, int order, int ns, T xcfl,
                T ycfl, int fma, int wait_from, const unsigned* flag, unsigned value, unsigned* timeout,
                hipStream_t s) {
-    if constexpr (sizeof(T) == 4)
+    if constexpr (sizeof(T) == 4) {
+        if (fma & kArithFast)
+            return cme_heat_pipe_fast_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, 0, wait_from, flag, value,
+                                          timeout, (void*)s);
         return cme_heat_pipe_gated_f32(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, fma & 1, wait_from, flag,
                                        value, timeout, (void*)s);
+    }
     else
         return cme_heat_pipe_gated_f64(p, c, pitch, gy, r, n, ext, order, ns, xcfl, ycfl, fma & 1, wait_from, flag,
                                        value, timeout, (void*)s);
@@ -868,6 +890,7 @@ int dist_run(int transport, ncclComm_t comm, const SubDesc* subs, int nsub, int 
     if (transport == 3 && (!subs[0].ipc || !subs[0].ipc->epoch)) return (int)hipErrorInvalidValue;
     if (tblock < 1 || tblock > 4 || (tblock > 3 && sizeof(T) != 4 && !(fma & kKernelPipe)))
         return (int)hipErrorInvalidValue;
+    if ((fma & kArithFast) && (sizeof(T) != 4 || order != 8)) return (int)hipErrorInvalidValue;
     // 2 (default, see `fused` below) where it applies, else 0: border stream
     // || interior stream; 1: border then interior on one stream. Measured on one N=8-rank subdomain (bench_dist_rank.py,
     // null transport): 0.041 vs 0.045 ms/step -- kept as a switch for

@@ -84,9 +84,11 @@ struct PipeN {
     static constexpr int NSLOT = LX ? 2 + B / RB : 2;  // ring slots per role hand-off
     // FMA: 0 exact, 1 FMA-contracted (the reference's nvcc -fmad code), 2 / 3
     // reassociated ("fast"; 3 capped at 4 waves/SIMD), 4 FMA-contracted with
-    // the chains of the lane's VW points interleaved term by term (bitwise 1)
-    static constexpr bool kFast = FMA == 2 || FMA == 3;
+    // the chains of the lane's VW points interleaved term by term (bitwise 1),
+    // 5 reassociated with the terms interleaved across the points (bitwise 2)
+    static constexpr bool kFast = FMA == 2 || FMA == 3 || FMA == 5;
     static constexpr bool kTermMajor = FMA == 4;
+    static constexpr bool kFastTM = FMA == 5;  // reassociated, terms issued across the lane's points
     using VT = VecN<T, VW>;
     using Ring = V4<T>[NSLOT][RB][NH][LW];
     using Edge = V4<T>[3][RB][WPR][2];
@@ -144,7 +146,36 @@ struct PipeN {
         bool row_in = true;
         if constexpr (MASK) row_in = row >= yb1 && row < ye1;
         VT o;
-        if constexpr (kTermMajor) {
+        if constexpr (kFastTM) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+            // heat_update_fast per point (c0 c, then the x pairs, then the y
+            // pairs, k = B-1..0), each term issued for all VW points first
+            T u[VW];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) u[j] = fc.c0 * c[j];
+#pragma unroll
+            for (int k = B - 1; k >= 0; --k)
+#pragma unroll
+                for (int j = 0; j < VW; ++j)
+                    u[j] = fmaT<T>(fc.ax[k], rowv[B + j + (k + 1)] + rowv[B + j - (k + 1)], u[j]);
+#pragma unroll
+            for (int k = B - 1; k >= 0; --k)
+#pragma unroll
+                for (int j = 0; j < VW; ++j)
+                    u[j] = fmaT<T>(fc.ay[k], w[(s_lo + B + (k + 1)) % NW][j] + w[(s_lo + B - (k + 1)) % NW][j], u[j]);
+#pragma unroll
+            for (int j = 0; j < VW; ++j) {
+                if constexpr (MASK) {
+                    const int x = xbase + j;
+                    o[j] = (row_in && x >= xb1 && x < xe1) ? u[j] : c[j];
+                } else {
+                    o[j] = u[j];
+                }
+            }
+            return o;
+        } else if constexpr (kTermMajor) {
             T cc[VW], xm[B][VW], xp[B][VW], ym[B][VW], yp[B][VW], dx[VW], dy[VW];
 #pragma unroll
             for (int j = 0; j < VW; ++j) {
@@ -370,7 +401,7 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
     st.ye1 = ye1;
     st.xcfl = xcfl;
     st.ycfl = ycfl;
-    if constexpr (FMA == 2 || FMA == 3) {
+    if constexpr (FMA == 2 || FMA == 3 || FMA == 5) {
         const HeatFast<ORDER, T> f = heat_fast_coefs<ORDER>(xcfl, ycfl);
         st.fc.c0 = uniform_f(f.c0);
 #pragma unroll

@@ -71,6 +71,21 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, 2, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                             chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 92:  // wide lanes, reassociated, registers capped for 3 waves per SIMD
+            if constexpr (RB == 2 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, 2, RB, 1, true, 1, 8, 3>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                               chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 95:  // wide lanes, reassociated, terms interleaved across the lane's points (bitwise = 91)
+            if constexpr (RB == 2 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, 5, RB, 1, true, 1, 8>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                            chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
+        case 96:  // the same, capped for 3 waves per SIMD
+            if constexpr (RB == 2 && NS <= 4)
+                return launch_pipe_multi<float, 8, NS, 5, RB, 1, true, 1, 8, 3>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                               chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
         case 84:
             if constexpr (RB == 2 && NS == 4) {

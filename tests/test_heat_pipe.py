@@ -268,7 +268,8 @@ def test_fast_oracle_close_to_exact():
 @pytest.mark.gpu
 def test_gpu_pipe_fast_arms_bitwise(gpu, tune_lib):
     """The reassociated-arithmetic tuning arms (pd 12: default registers, 13:
-    capped at 4 waves/SIMD, 91: wide lanes) equal ns steps of the CPU fast
+    capped at 4 waves/SIMD, 91: wide lanes, 92: capped at 3 waves/SIMD, 95 / 96:
+    terms interleaved across the lane's points) equal ns steps of the CPU fast
     oracle bit for bit."""
     from cme213x import _ext
     p = SimParams(nx=1500, ny=700, order=8)
@@ -278,7 +279,7 @@ def test_gpu_pipe_fast_arms_bitwise(gpu, tune_lib):
     s = _ext.stream_ptr(g.buf[0].device)
     for ns in (3, 4):
         oracle = _fast_steps(c, region, ns)
-        for pd, rb in ((12, 4), (13, 4), (91, 2)):  # 91: wide lanes
+        for pd, rb in ((12, 4), (13, 4), (91, 2), (92, 2), (95, 2), (96, 2)):  # 9x: wide lanes
             out = g.buf[0].clone()
             _ext.call_hip("cme_heat_pipe_tune", g.buf[0].data_ptr(), out.data_ptr(), g.pitch, g.gy, *region,
                           g.xcfl, g.ycfl, 0, rb, ns, pd, 0, s)

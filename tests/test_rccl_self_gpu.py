@@ -75,7 +75,14 @@ CASES = [
     (2, (True, True), 4, False, "float32", "pipe", False),
     (2, (True, False), 3, True, "float64", "pipe", True),       # columns only, fp64, fused
     (1, (False, True), 4, True, "float64", "pipe", True),
+    (1, (False, True), 4, "fast", "float32", "pipe", True),     # reassociated arithmetic, fused
+    (2, (True, True), 4, "fast", "float32", "pipe", True),
+    (2, (True, True), 3, "fast", "float32", "pipe", False),
 ]
+
+
+def _arith_name(fma):
+    return "fast" if fma == "fast" else ("fma" if fma else "exact")
 
 
 def _run_case(case, group=None):
@@ -103,7 +110,7 @@ def _run_case(case, group=None):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"m{c[0]}-p{int(c[1][0])}{int(c[1][1])}-t{c[2]}-"
-                                                         f"{'fma' if c[3] else 'exact'}-{c[4]}-{c[5]}"
+                                                         f"{_arith_name(c[3])}-{c[4]}-{c[5]}"
                                                          f"{'-fused' if c[6] else '-sched0'}")
 def test_rccl_self_peer_halo_bitwise(gpu, case):
     import torch.distributed as dist

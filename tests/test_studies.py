@@ -63,6 +63,9 @@ def test_gpu_tree_reduction_beats_serial(gpu):
     assert r["gpu_tree"] < r["serial"] and r["gpu_vector"] < r["serial"]
 
 
+_SPILL_OK = {"heat_pipe4w_fast_f32_o8": 64}
+
+
 @pytest.mark.gpu
 def test_occupancy_report(gpu):
     from cme213x.utils.occupancy import format_report, kernel_report
@@ -73,5 +76,7 @@ def test_occupancy_report(gpu):
     for r in rows:
         assert r["blocks_per_cu"] >= 1, r
         assert 0 < r["vgprs"] <= 512, r
-        assert r["scratch_bytes"] == 0, f"{r['kernel']} spills to scratch"
+        # the reassociated 4-step pass is capped at 3 waves per SIMD, which
+        # costs 32 B/lane of scratch and still wins (csrc/hip/heat_fast.hip)
+        assert r["scratch_bytes"] <= _SPILL_OK.get(r["kernel"], 0), f"{r['kernel']} spills to scratch"
     assert "heat_stream2_f32_o8" in format_report(rows)
