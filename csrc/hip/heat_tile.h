@@ -123,7 +123,13 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
 
 template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
 __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
-                                                       int gy, Region g, int tiles_x, T xcfl, T ycfl) {
+                                                       int gy, Region g, int tiles_x, T xcfl, T ycfl,
+                                                       unsigned long long* __restrict__ trace) {
+    // trace (profiling only, benchmarks/trace_tile.py): thread 0 of each
+    // workgroup records the wall clock at entry, after the load, after each
+    // step and after its stores -- trace[8 * block + 0 .. NS + 2]
+    unsigned long long tr[8];
+    if (trace && threadIdx.x == 0) tr[0] = wall_clock64();
     using G = TileGeom<T, ORDER, NS, TX, TY>;
     constexpr int B = G::B, H = G::H, PW = G::PW, LW = G::LW, LH = G::LH;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -138,7 +144,10 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     // batches of kLB per thread, all issued before their LDS stores, so the
     // memory latency is paid once per batch, not once per element.
     constexpr int kN = LH * LW;
-    constexpr int kLB = 8;
+    // every load of the tile in flight at once where it fits (9 per thread
+    // for the production 64 x 64, NS = 4, 1024-thread shape: one memory
+    // latency instead of two; the trace had the 8-per-batch load at 2.2 us)
+    constexpr int kLB = (kN + NT - 1) / NT < 16 ? (kN + NT - 1) / NT : 16;
     for (int i0 = 0; i0 < kN; i0 += NT * kLB) {
         T v[kLB];
 #pragma unroll
@@ -159,6 +168,7 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
         }
     }
     __syncthreads();
+    if (trace && threadIdx.x == 0) tr[1] = wall_clock64();
     // region g in LDS coordinates
     const int gxl = g.xb - gx0, gxh = g.xe - gx0, gyl = g.yb - gy0, gyh = g.ye - gy0;
 #pragma unroll
@@ -168,20 +178,27 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
         const int r_lo = max(H - e, gyl), r_hi = min(H + TY + e, gyh);
         tile_step<T, ORDER, FMA, PW, NT>((s & 1) ? L0 : L1, (s & 1) ? L1 : L0, c_lo, c_hi, r_lo, r_hi, xcfl, ycfl);
         __syncthreads();
+        if (trace && threadIdx.x == 0) tr[1 + s] = wall_clock64();
     }
     const T* fin = (NS & 1) ? L1 : L0;
     const int c_lo = max(H, gxl), c_hi = min(H + TX, gxh);
     const int r_lo = max(H, gyl), r_hi = min(H + TY, gyh);
     const int w = c_hi - c_lo;
-    if (w <= 0 || r_hi <= r_lo) return;
-    for (int i = threadIdx.x; i < w * (r_hi - r_lo); i += NT) {
-        const int r = r_lo + i / w, c = c_lo + i % w;
-        curr[(size_t)(gy0 + r) * pitch + gx0 + c] = fin[r * PW + c];
+    if (w > 0 && r_hi > r_lo) {
+        for (int i = threadIdx.x; i < w * (r_hi - r_lo); i += NT) {
+            const int r = r_lo + i / w, c = c_lo + i % w;
+            curr[(size_t)(gy0 + r) * pitch + gx0 + c] = fin[r * PW + c];
+        }
+    }
+    if (trace && threadIdx.x == 0) {  // vector stores (lane 0)
+        tr[NS + 2] = wall_clock64();
+        for (int i = 0; i < NS + 3; ++i) trace[8ull * blockIdx.x + i] = tr[i];
     }
 }
 
 template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
-int launch_tile(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, hipStream_t s) {
+int launch_tile(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, hipStream_t s,
+                unsigned long long* trace = nullptr) {
     using G = TileGeom<T, ORDER, NS, TX, TY>;
     auto k = heat_tile_kernel<T, ORDER, NS, FMA, TX, TY, NT>;
     static const hipError_t attr =
@@ -190,7 +207,7 @@ int launch_tile(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T y
     const int W = g.xe - g.xb, Hh = g.ye - g.yb;
     if (W <= 0 || Hh <= 0) return 0;
     const int tx = (W + TX - 1) / TX, ty = (Hh + TY - 1) / TY;
-    hipLaunchKernelGGL(k, dim3(tx * ty), dim3(NT), G::kBytes, s, prev, curr, pitch, gy, g, tx, xcfl, ycfl);
+    hipLaunchKernelGGL(k, dim3(tx * ty), dim3(NT), G::kBytes, s, prev, curr, pitch, gy, g, tx, xcfl, ycfl, trace);
     return (int)hipGetLastError();
 }
 
