@@ -28,12 +28,19 @@ def main() -> int:
     ap.add_argument("--n", type=int, nargs="+", default=[1000, 2000])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fma", action="store_true", help="FMA-contracted stencil (the driver default is exact)")
+    ap.add_argument("--tune", nargs="*", default=[],
+                    help="tuning knobs name=value (cme213x.utils.tuning), e.g. pipe_per_cu=2")
     a = ap.parse_args()
 
     import torch
 
     import cme213x  # noqa: F401
     from cme213x.models.heat2d_dist import run_hw5
+    from cme213x.utils import tuning
+
+    knobs = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in a.tune}
+    for k, v in knobs.items():
+        tuning.set(k, v)
 
     src = open(os.path.join(REPO, "tests", "data", "hw5_params.in")).read().split("\n")
     for n in a.n:
@@ -55,6 +62,7 @@ def main() -> int:
         secs.sort()
         s = secs[len(secs) // 2]
         print(json.dumps({"bench": "hw5", "n": n, "order": 8, "iters": 1000, "dtype": "fp64", "ranks": 1, **info,
+                          "tune": knobs,
                           "seconds": round(s, 5), "ms": round(s * 1e3, 3), "ref_s": REF_S.get(n),
                           "speedup_vs_ref": round(REF_S[n] / s, 1) if n in REF_S else None}), flush=True)
     return 0
