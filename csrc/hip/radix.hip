@@ -31,6 +31,12 @@
 // Grid: co-resident (occupancy API - 1 blocks per CU), block b owns tiles
 // b, b+G, ... in order, so every predecessor of a tile belongs to a running
 // block: the smallest unfinished tile always progresses (no ticket counter).
+// (Round 4 measured the remedy the round-3 review proposed -- one workgroup
+// per tile, tile ids from a per-pass ticket so look-back predecessors are
+// always earlier-dispatched: 16M int32 0.84 ms vs 0.73 for this grid, 48M
+// 2.36 vs 2.14; profiles/sort_r4.md.) In-tile ranks: one returning LDS
+// atomic per key where the device resolves same-address lanes in lane order
+// (sort.hip kRankLanes, cme_radix_lane_order), else the ballot match.
 // Spins are bounded (lookback.h lb_give_up: sticky timeout word).
 //
 // Keys: uint32, int32 (sign bit flipped) or float32 (IEEE order flip) --
@@ -39,6 +45,10 @@
 #include "cme213/common.h"
 #include "cme213/lookback.h"
 #include "cme213/wave.h"
+
+// sort.hip: 1 if this device's returning LDS atomics resolve same-address
+// lanes in lane order (checked once per device when `check`)
+extern "C" int cme_radix_lane_order(int check);
 
 using namespace cme;
 
@@ -134,7 +144,7 @@ __device__ __forceinline__ uint64_t os_match(uint32_t d, bool valid) {
 }
 
 // ---------------------------------------------------------------- K1..KP
-template <bool HAS_VALUES>
+template <bool HAS_VALUES, bool LANES>
 __global__ __launch_bounds__(kOsThreads, HAS_VALUES ? 2 : 4) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ vout, long long n, int shift, int mode_in, int mode_out,
@@ -177,19 +187,46 @@ __global__ __launch_bounds__(kOsThreads, HAS_VALUES ? 2 : 4) void radix_onesweep
             for (int k = 0; k < kOsItems; ++k) key[k] = k < nk ? key_in(key[k], mode_in) : key[k];
         }
         __syncthreads();  // counters zeroed; previous tile's LDS reads done
-        // stable in-tile ranks: (wave, item, lane) is memory order. The
-        // scheduling barriers keep the compiler from hoisting every item's
-        // 8 ballots (64-bit masks) above the LDS chain (register spills).
+        // stable in-tile ranks: (wave, item, lane) is memory order
+        if constexpr (LANES) {
+            // one returning LDS atomic per key (lanes resolve in lane order);
+            // a wave whose valid keys share one digit adds once
 #pragma unroll
-        for (int k = 0; k < kOsItems; ++k) {
-            const bool ok = k < nk;
-            const uint32_t d = (key[k] >> shift) & 255u;
-            const uint64_t peers = os_match(d, ok);
-            const uint32_t below = (uint32_t)__builtin_popcountll(peers & lt);
-            const uint32_t prev = ok ? s_cnt[wid][d] : 0u;
-            rank[k] = ok ? prev + below : 0xffffffffu;
-            if (ok && below == 0) s_cnt[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int k = 0; k < kOsItems; ++k) {
+                const bool ok = k < nk;
+                const uint32_t d = (key[k] >> shift) & 255u;
+                const uint64_t act = __ballot(ok);
+                if (act == 0) {
+                    rank[k] = 0xffffffffu;
+                    continue;
+                }
+                const int first = (int)__builtin_ctzll(act);
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+                if (__ballot(ok && d != d0) == 0) {
+                    uint32_t base = 0;
+                    if (lane == first) base = atomicAdd(&s_cnt[wid][d0], (uint32_t)__builtin_popcountll(act));
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
+                    rank[k] = ok ? base + (uint32_t)__builtin_popcountll(act & lt) : 0xffffffffu;
+                } else {
+                    uint32_t old = 0xffffffffu;
+                    if (ok) old = atomicAdd(&s_cnt[wid][d], 1u);
+                    rank[k] = old;
+                }
+            }
+        } else {
+            // ballot match; the scheduling barriers keep the compiler from
+            // hoisting every item's 8 ballots above the LDS chain (spills)
+#pragma unroll
+            for (int k = 0; k < kOsItems; ++k) {
+                const bool ok = k < nk;
+                const uint32_t d = (key[k] >> shift) & 255u;
+                const uint64_t peers = os_match(d, ok);
+                const uint32_t below = (uint32_t)__builtin_popcountll(peers & lt);
+                const uint32_t prev = ok ? s_cnt[wid][d] : 0u;
+                rank[k] = ok ? prev + below : 0xffffffffu;
+                if (ok && below == 0) s_cnt[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         if constexpr (HAS_VALUES) {  // values are only needed for the reorder: loaded after the ranking
 #pragma unroll
@@ -374,8 +411,13 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
     // waves per SIMD = 2 blocks of 8 waves); the SGPR file (106 per wave: 6
     // waves per SIMD) does not, so the API's known over-report for SGPR-bound
     // kernels (common.h persistent_blocks_per_cu) does not apply here.
-    static const int bpc_k = occupancy_blocks_per_cu(radix_onesweep_kernel<false>, kOsThreads);
-    static const int bpc_kv = occupancy_blocks_per_cu(radix_onesweep_kernel<true>, kOsThreads);
+    static const int bpc_k = occupancy_blocks_per_cu(radix_onesweep_kernel<false, true>, kOsThreads);
+    static const int bpc_kv = occupancy_blocks_per_cu(radix_onesweep_kernel<true, true>, kOsThreads);
+    // lane-order ranks where the device passed the check (not checked under
+    // stream capture: a device not yet checked takes the ballot match)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+    const bool lanes = cme_radix_lane_order(capturing ? 0 : 1) != 0;
     const long long cap = (long long)device_cu_count() * (vin ? bpc_kv : bpc_k);
     const int grid = (int)(tiles < cap ? tiles : cap);
     const uint32_t* src = kin;
@@ -388,12 +430,21 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
         const int shift = bit0 + 8 * p;
         const uint32_t tag = (uint32_t)(epoch * kMaxPasses + p);
         const int mi = p == 0 ? mode : 0, mo = p == npass - 1 ? mode : 0;
-        if (vin)
-            hipLaunchKernelGGL(radix_onesweep_kernel<true>, dim3(grid), dim3(kOsThreads), 0, s, src, dst, vsrc, vdst,
-                               n, shift, mi, mo, hist + p * kBins, agg, inc, stat, (int)tiles, tag, timeout);
-        else
-            hipLaunchKernelGGL(radix_onesweep_kernel<false>, dim3(grid), dim3(kOsThreads), 0, s, src, dst, vsrc,
-                               vdst, n, shift, mi, mo, hist + p * kBins, agg, inc, stat, (int)tiles, tag, timeout);
+#define CME_OS(V, L)                                                                                            \
+    hipLaunchKernelGGL((radix_onesweep_kernel<V, L>), dim3(grid), dim3(kOsThreads), 0, s, src, dst, vsrc, vdst, n, \
+                       shift, mi, mo, hist + p * kBins, agg, inc, stat, (int)tiles, tag, timeout)
+        if (vin) {
+            if (lanes)
+                CME_OS(true, true);
+            else
+                CME_OS(true, false);
+        } else {
+            if (lanes)
+                CME_OS(false, true);
+            else
+                CME_OS(false, false);
+        }
+#undef CME_OS
         CME_TRY(hipGetLastError());
         src = dst;
         vsrc = vdst;
@@ -402,5 +453,5 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
 }
 
 CME_REGISTER_KERNEL(radix_hist, 256, radix_hist_kernel);
-CME_REGISTER_KERNEL(radix_onesweep, 512, radix_onesweep_kernel<false>);
-CME_REGISTER_KERNEL(radix_onesweep_kv, 512, radix_onesweep_kernel<true>);
+CME_REGISTER_KERNEL(radix_onesweep, 512, radix_onesweep_kernel<false, true>);
+CME_REGISTER_KERNEL(radix_onesweep_kv, 512, radix_onesweep_kernel<true, true>);
