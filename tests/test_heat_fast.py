@@ -57,13 +57,15 @@ def test_fast_refused_outside_fp32_order8_pipe():
         heat_stepn(g.buf[0], g.buf[1], g.interior, g.interior, 4, g.xcfl, g.ycfl, 3, fma="fast")
 
 
-@pytest.mark.parametrize("world,method,tblock", [(4, 1, 1), (4, 2, 2), (2, 1, 4)])
+@pytest.mark.parametrize("world,method,tblock", [(4, 1, 1), (4, 2, 2), (2, 1, 4), (8, 1, 4)])
 def test_fast_loopback_subdomains_cpu(world, method, tblock):
     """CPU: the distributed solver with reassociated arithmetic over loopback
     subdomains equals the single-grid fast run bit for bit."""
     from cme213x.models.heat2d_dist import DistHeat
 
-    p = SimParams(nx=97, ny=83, order=8, iters=6, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
+    # (8 stripes of 40 rows: the bench's 8-way split, four steps per pass, 16-row halos -- in one process)
+    ny = 320 if world == 8 else 83
+    p = SimParams(nx=97, ny=ny, order=8, iters=6, ic=5.0, bc=(1.0, 10.0, 3.0, 7.0), grid_method=method,
                   flavor="hw5")
     one = DistHeat(p, None, torch.float32, "cpu", fma="fast")
     many = DistHeat(p, None, torch.float32, "cpu", fma="fast", tblock=tblock, local_ranks=list(range(world)),
