@@ -37,6 +37,9 @@ def heat2d_mpi_main(argv=None) -> int:
     ap.add_argument("--kernel", default="auto", choices=["auto", "pipe", "streamn", "tile"],
                     help="multi-step pass kernel (tile: LDS-resident tiles, single-grid runs)")
     ap.add_argument("--fma", action="store_true", help="FMA-contracted stencil (the reference CPU's is not)")
+    ap.add_argument("--fast", action="store_true",
+                    help="reassociated stencil (folded CFL weights, pair sums; within 10 ULP of exact): fp32 "
+                         "(--float) order 8 multi-step passes, csrc/hip/heat_fast.hip")
     ap.add_argument("--native", default="auto", choices=["auto", "on", "off"],
                     help="GPU time loop: the native C++ loop after a bitwise self-test (auto), required (on), "
                          "or the Python loop (off)")
@@ -52,11 +55,12 @@ def heat2d_mpi_main(argv=None) -> int:
     tblock = a.tblock if a.tblock == "auto" else int(a.tblock)
     dtype = torch.float32 if a.float else torch.float64
     periodic = ("x" in a.periodic, "y" in a.periodic)
+    fma = "fast" if a.fast else a.fma
     if a.ranks:
-        run_hw5(a.params, None, dtype, a.device, tblock=tblock, fma=a.fma, kernel=a.kernel, native=a.native,
+        run_hw5(a.params, None, dtype, a.device, tblock=tblock, fma=fma, kernel=a.kernel, native=a.native,
                 local_ranks=list(range(a.ranks)), world=a.ranks, periodic=periodic)
         return 0
     comm = init_from_env(backend="gloo" if a.share_gpu else None, share_gpu=a.share_gpu)
-    run_hw5(a.params, comm, dtype, a.device, tblock=tblock, fma=a.fma, kernel=a.kernel, native=a.native,
+    run_hw5(a.params, comm, dtype, a.device, tblock=tblock, fma=fma, kernel=a.kernel, native=a.native,
             periodic=periodic, transport=a.transport or ("ipc" if a.share_gpu else None))
     return 0

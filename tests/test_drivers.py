@@ -25,6 +25,21 @@ def test_heat2d_mpi_loopback(in_tmp, capsys):
     assert all(os.path.exists(f"grid{r}_final.txt") for r in range(4))
 
 
+def test_heat2d_mpi_fast_arithmetic(in_tmp, capsys):
+    """--fast (reassociated stencil, fp32, order 8) runs through the driver
+    (bitwise equality of the decomposed run: test_heat_fast.py); other
+    orders / fp64 are refused."""
+    with open("params.in", "w") as f:
+        f.write("60 72\n1 1\n1\n6\n8\n5\n1\n0\n0 10 0 10\n")
+    assert main(["heat2d_mpi", "params.in", "--ranks", "4", "--device", "cpu", "--float", "--fast"]) == 0
+    assert "6 iterations on a 60 by 72 grid took:" in capsys.readouterr().out
+    assert all(os.path.exists(f"grid{r}_final.txt") for r in range(4))
+    with open("params.in", "w") as f:
+        f.write("60 72\n1 1\n1\n6\n4\n5\n1\n0\n0 10 0 10\n")
+    with pytest.raises(ValueError, match="fast"):
+        main(["heat2d_mpi", "params.in", "--ranks", "2", "--device", "cpu", "--float", "--fast", "--tblock", "2"])
+
+
 def test_heat2d_cpu(in_tmp):
     with open("params.in", "w") as f:
         f.write("50 30\n1 1\n1\n3\n8\n5\n0 10 0 10\n")

@@ -142,7 +142,7 @@ def test_gpu_fast_heat_run_bitwise(gpu, variant, iters):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method,world", [(1, 4), (2, 4), (1, 3)])
+@pytest.mark.parametrize("method,world", [(1, 4), (2, 4), (1, 3), (1, 8)])
 @pytest.mark.parametrize("sync", [False, True])
 @pytest.mark.parametrize("tblock", [3, 4])
 @pytest.mark.parametrize("native", [True, False])

@@ -259,14 +259,16 @@ def test_run_hw5_fused_selftest_failure_falls_back_to_schedule0(gpu, tmp_path, m
 
 
 @pytest.mark.gpu
-def test_heat2d_mpi_ranks_uses_native_loop(gpu, tmp_path, monkeypatch, capsys):
+@pytest.mark.parametrize("arith", ["--fma", "--fast"])
+def test_heat2d_mpi_ranks_uses_native_loop(gpu, tmp_path, monkeypatch, capsys, arith):
     """heat2d_mpi --ranks 2 on the GPU runs the native loop (loopback
-    transport) after its self-test and logs it."""
+    transport) after its self-test and logs it (FMA-contracted and
+    reassociated arithmetic)."""
     from cme213x.__main__ import main
 
     monkeypatch.chdir(tmp_path)
     (tmp_path / "params.in").write_text("300 200\n1 1\n1\n9\n8\n5\n1\n0\n0 10 0 10\n")
-    assert main(["heat2d_mpi", "params.in", "--ranks", "2", "--float", "--fma", "--tblock", "4",
+    assert main(["heat2d_mpi", "params.in", "--ranks", "2", "--float", arith, "--tblock", "4",
                  "--kernel", "pipe"]) == 0
     out = capsys.readouterr().out
     assert "time loop: native (loopback transport, bitwise self-test passed" in out, out
