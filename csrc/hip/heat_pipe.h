@@ -463,11 +463,16 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the halo rows the exchange wrote, not stale L1 lines
     }
     const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
-    const int strips = R.strips[r], chunk = R.chunk[r];
+    const int strips = R.strips[r];
+    // chunk word: rows per chunk in the low 16 bits; a tapered region
+    // (pipe_taper) keeps n1 = bits 16.. full chunks per strip and cuts the
+    // rest -- the tasks dispatched last -- to half height
+    const int chunk = R.chunk[r] & 0xffff, n1 = R.chunk[r] >> 16;
     const int strip = task % strips;
     const int ck = task / strips;
-    const int y0 = yb + ck * chunk;
-    const int y1 = min(ye, y0 + chunk);
+    const bool half = n1 > 0 && ck >= n1;
+    const int y0 = half ? yb + n1 * chunk + (ck - n1) * (chunk >> 1) : yb + ck * chunk;
+    const int y1 = min(ye, y0 + (half ? chunk >> 1 : chunk));
     const int xs = (xb & ~(VW - 1)) + strip * OUT;
     const int gl = sub * 64 + lane;
     const int xbase = xs - VW * M + VW * gl;
@@ -587,12 +592,29 @@ int launch_pipe_multi(const T* prev, T* curr, int pitch, int gy, const Region* g
         if (i >= gate_from && gate.from == kMaxS2Regions) gate.from = R.n;
         if (H <= 0 || g.xe <= g.xb) continue;
         const int strips = (int)cdiv(g.xe - (g.xb & ~(VW - 1)), kOut);
-        const int chunk = pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, n > 1, reserve);
+        int chunk = pipe_chunk<NS, RB, VW>(strips, H, chunk_hint, per_cu, resident, n > 1, reserve);
+        int nchunks = (int)cdiv(H, chunk), n1 = 0;
+        // taper (pipe_taper): a region of several rounds of resident tasks
+        // ends in shorter tasks, so the last round drains sooner (the
+        // per-task trace had the N = 1 pass at 84 % slot utilisation,
+        // profiles/dist_rank_trace_r4.md). m2 half-height chunks per strip
+        // (-1: enough to fill one round of the resident workgroups)
+        const long taper = cme::tune_get(cme::kTunePipeTaper);
+        if (taper != 0 && chunk_hint <= 0 && (long)strips * nchunks > 2 * resident) {
+            const int c1 = ((chunk + 2 * RB - 1) / (2 * RB)) * (2 * RB), c2 = c1 / 2;
+            const long m2 = taper > 0 ? taper : cdiv(resident, strips);
+            const long full = ((long)H - m2 * c2) / c1;
+            if (full >= 1 && c1 < 65536) {
+                n1 = (int)full;
+                chunk = c1;
+                nchunks = n1 + (int)cdiv(H - n1 * c1, c2);
+            }
+        }
         const int k = R.n++;
         R.xb[k] = g.xb, R.xe[k] = g.xe, R.yb[k] = g.yb, R.ye[k] = g.ye;
         R.strips[k] = strips;
-        R.chunk[k] = chunk;
-        tasks += strips * (int)cdiv(H, chunk);
+        R.chunk[k] = chunk | (n1 << 16);
+        tasks += strips * nchunks;
         R.wave_end[k] = tasks;
     }
     if (R.n == 0) return 0;

@@ -316,3 +316,24 @@ def test_dist_heat_kernel_option_cpu():
     a.run(5)
     b.run(5)
     assert np.array_equal(a.gather_global(), b.gather_global())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["pipe4_fma", "pipe4_fast", "pipe3_fma"])
+@pytest.mark.parametrize("taper", [-1, 7])
+def test_gpu_pipe_taper_bitwise(gpu, variant, taper):
+    """Tapered chunking (tuning knob pipe_taper: the last chunks of every
+    strip at half height, for passes of several rounds of workgroups) only
+    moves task boundaries: bitwise equal to the untapered pass."""
+    from cme213x.ops.stencil import heat_run
+    from cme213x.utils import tuning
+
+    p = SimParams(nx=4000, ny=3000, order=8)
+    g = _rand_grid(p, torch.float32, gpu, seed=11)
+    outs = []
+    for t in (0, taper):
+        with tuning.override(pipe_per_cu=16, pipe_taper=t):  # 16 tasks per CU: several rounds
+            a, b = g.buf[0].clone(), g.buf[1].clone()
+            outs.append(heat_run(a, b, g.interior, 8, g.xcfl, g.ycfl, 9, variant).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
