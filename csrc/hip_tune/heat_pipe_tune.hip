@@ -86,6 +86,11 @@ int tunep_pd(const float* p, float* c, int pitch, int gy, Region g, float xcfl, 
                 return launch_pipe_multi<float, 8, NS, 5, RB, 1, true, 1, 8, 3>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
                                                                                chunk, per_cu, s);
             return (int)hipErrorInvalidValue;
+        case 97:  // wide lanes, reassociated term-major, ONE row per phase, 3 waves per SIMD (168 VGPRs, no spill)
+            if constexpr (RB == 1 && NS == 4)
+                return launch_pipe_multi<float, 8, NS, 5, RB, 1, true, 1, 8, 3>(p, c, pitch, gy, &g, 1, g, xcfl, ycfl,
+                                                                               chunk, per_cu, s);
+            return (int)hipErrorInvalidValue;
         case 83:  // wide lanes, registers capped for 3 / 4 waves per SIMD
         case 84:
             if constexpr (RB == 2 && NS == 4) {
