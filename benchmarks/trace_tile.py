@@ -23,6 +23,7 @@ def main() -> int:
     ap.add_argument("--n", type=int, nargs="+", default=[1000])
     ap.add_argument("--ns", type=int, default=4)
     ap.add_argument("--fma", type=int, nargs="+", default=[0, 1])
+    ap.add_argument("--nts", type=int, nargs="+", default=[0], help="1: non-temporal output stores")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -32,7 +33,7 @@ def main() -> int:
     from cme213x.models.heat2d import HeatGrid
     from cme213x.utils.params import SimParams
 
-    _ext.proto(_ext.TUNE_PROTOS, "cme_heat_tile_trace", "ppiiiiiiiiddpp")
+    _ext.proto(_ext.TUNE_PROTOS, "cme_heat_tile_trace", "ppiiiiiiiiiddpp")
     mhz = 100.0  # wall_clock64 rate on gfx950
     for n in args.n:
         p = SimParams(nx=n, ny=n, order=8, ic=3.0, bc=(0.0, 10.0, 0.0, 10.0))
@@ -42,10 +43,10 @@ def main() -> int:
         g.buf[:, B:B + n, B:B + n] = torch.rand((n, n), generator=gen, device="cuda", dtype=torch.float64) * 10
         tiles = ((n + 63) // 64) ** 2
         tr = [torch.zeros(8 * tiles, dtype=torch.int64, device="cuda") for _ in range(2)]
-        for fma in args.fma:
+        for fma, nts in [(f, m) for f in args.fma for m in args.nts]:
             def one(k, t):
                 _ext.call_hip("cme_heat_tile_trace", g.buf[k].data_ptr(), g.buf[1 - k].data_ptr(), g.pitch, g.gy,
-                              *g.interior, args.ns, fma, g.xcfl, g.ycfl, t.data_ptr() if t is not None else None,
+                              *g.interior, args.ns, fma, nts, g.xcfl, g.ycfl, t.data_ptr() if t is not None else None,
                               _ext.stream_ptr())
 
             t_end = time.perf_counter() + 1.0  # clock ramp
@@ -71,7 +72,7 @@ def main() -> int:
                     ph[f"step{s}"] = x[:, 1 + s] - x[:, s]
                 ph["store"] = x[:, ns + 2] - x[:, ns + 1]
                 ph["workgroup"] = x[:, ns + 2] - x[:, 0]
-                rec = {"bench": "tile_trace", "n": n, "ns": ns, "fma": fma, "pass": pi, "tiles": tiles,
+                rec = {"bench": "tile_trace", "n": n, "ns": ns, "fma": fma, "nts": nts, "pass": pi, "tiles": tiles,
                        "span_us": round(float(x[:, ns + 2].max() - x[:, 0].min()) / mhz, 2),
                        "start_spread_us": round(float(x[:, 0].max() - x[:, 0].min()) / mhz, 2)}
                 for k, v in ph.items():

@@ -121,7 +121,8 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
     }
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
+// NTS: non-temporal output stores
+template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT, bool NTS = false>
 __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ prev, T* __restrict__ curr, int pitch,
                                                        int gy, Region g, int tiles_x, T xcfl, T ycfl,
                                                        unsigned long long* __restrict__ trace) {
@@ -187,7 +188,11 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     if (w > 0 && r_hi > r_lo) {
         for (int i = threadIdx.x; i < w * (r_hi - r_lo); i += NT) {
             const int r = r_lo + i / w, c = c_lo + i % w;
-            curr[(size_t)(gy0 + r) * pitch + gx0 + c] = fin[r * PW + c];
+            T* d = curr + (size_t)(gy0 + r) * pitch + gx0 + c;
+            if constexpr (NTS)
+                __builtin_nontemporal_store(fin[r * PW + c], d);
+            else
+                *d = fin[r * PW + c];
         }
     }
     if (trace && threadIdx.x == 0) {  // vector stores (lane 0)
@@ -196,11 +201,11 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     }
 }
 
-template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT>
+template <typename T, int ORDER, int NS, bool FMA, int TX, int TY, int NT, bool NTS = false>
 int launch_tile(const T* prev, T* curr, int pitch, int gy, Region g, T xcfl, T ycfl, hipStream_t s,
                 unsigned long long* trace = nullptr) {
     using G = TileGeom<T, ORDER, NS, TX, TY>;
-    auto k = heat_tile_kernel<T, ORDER, NS, FMA, TX, TY, NT>;
+    auto k = heat_tile_kernel<T, ORDER, NS, FMA, TX, TY, NT, NTS>;
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::kBytes);
     if (attr != hipSuccess) return (int)attr;

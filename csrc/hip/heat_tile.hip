@@ -32,13 +32,16 @@ constexpr int kTileThreads = 1024;  // 16 waves: 4 per SIMD (tune_tile.py cfg 2)
 // Tile shapes: fp64 64 x 64 (1000^2 = 256 tiles, one workgroup per CU; LDS
 // 2 x (64 + 2NSB)^2 x 8 B = 102 / 124 / 147 KB at NS = 2 / 3 / 4); fp32
 // 64 x 64 as well (half the LDS: two workgroups per CU up to NS = 4).
+// Output tiles go out with non-temporal stores: the kernel boundary after a
+// pass shrinks (3.8 -> 3.2 us) and a 1000^2 pass runs 19.8 -> 18.7 us exact,
+// 17.1 -> 16.1 FMA (benchmarks/trace_tile.py, profiles/heat_tile_r4.md).
 template <typename T, int ORDER, bool FMA>
 int tile_ns(const T* p, T* c, int pitch, int gy, Region g, int ns, T xcfl, T ycfl, hipStream_t s) {
     switch (ns) {
-        case 1: return cme_tile::launch_tile<T, ORDER, 1, FMA, 64, 64, kTileThreads>(p, c, pitch, gy, g, xcfl, ycfl, s);
-        case 2: return cme_tile::launch_tile<T, ORDER, 2, FMA, 64, 64, kTileThreads>(p, c, pitch, gy, g, xcfl, ycfl, s);
-        case 3: return cme_tile::launch_tile<T, ORDER, 3, FMA, 64, 64, kTileThreads>(p, c, pitch, gy, g, xcfl, ycfl, s);
-        case 4: return cme_tile::launch_tile<T, ORDER, 4, FMA, 64, 64, kTileThreads>(p, c, pitch, gy, g, xcfl, ycfl, s);
+        case 1: return cme_tile::launch_tile<T, ORDER, 1, FMA, 64, 64, kTileThreads, true>(p, c, pitch, gy, g, xcfl, ycfl, s);
+        case 2: return cme_tile::launch_tile<T, ORDER, 2, FMA, 64, 64, kTileThreads, true>(p, c, pitch, gy, g, xcfl, ycfl, s);
+        case 3: return cme_tile::launch_tile<T, ORDER, 3, FMA, 64, 64, kTileThreads, true>(p, c, pitch, gy, g, xcfl, ycfl, s);
+        case 4: return cme_tile::launch_tile<T, ORDER, 4, FMA, 64, 64, kTileThreads, true>(p, c, pitch, gy, g, xcfl, ycfl, s);
         default: return (int)hipErrorInvalidValue;
     }
 }

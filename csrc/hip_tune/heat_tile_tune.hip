@@ -65,14 +65,19 @@ CME_EXPORT int cme_heat_tile_tune(double* a, double* b, int pitch, int gy, int x
 // One ns-step pass of the production tile shape (64 x 64, 1024 threads) with
 // per-workgroup phase timestamps (heat_tile.h trace: entry, load, each step,
 // stores; 8 words per workgroup, 100 MHz wall clock).
+// nts: non-temporal output stores.
 CME_EXPORT int cme_heat_tile_trace(const double* a, double* b, int pitch, int gy, int xb, int xe, int yb, int ye,
-                                   int ns, int fma, double xcfl, double ycfl, unsigned long long* trace,
+                                   int ns, int fma, int nts, double xcfl, double ycfl, unsigned long long* trace,
                                    void* stream) {
     using namespace cme_tile;
     const Region g{xb, xe, yb, ye};
     hipStream_t s = as_stream(stream);
-#define CME_TT(NS)                                                                                            \
-    return fma ? launch_tile<double, 8, NS, true, 64, 64, 1024>(a, b, pitch, gy, g, xcfl, ycfl, s, trace)  \
+#define CME_TT(NS)                                                                                                 \
+    if (nts)                                                                                                      \
+        return fma ? launch_tile<double, 8, NS, true, 64, 64, 1024, true>(a, b, pitch, gy, g, xcfl, ycfl, s, trace) \
+                   : launch_tile<double, 8, NS, false, 64, 64, 1024, true>(a, b, pitch, gy, g, xcfl, ycfl, s,      \
+                                                                              trace);                              \
+    return fma ? launch_tile<double, 8, NS, true, 64, 64, 1024>(a, b, pitch, gy, g, xcfl, ycfl, s, trace)       \
                : launch_tile<double, 8, NS, false, 64, 64, 1024>(a, b, pitch, gy, g, xcfl, ycfl, s, trace)
     switch (ns) {
         case 2: CME_TT(2);
