@@ -17,25 +17,45 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+SINGLE = {}  # last measurement's one-call-per-event-pair median (ms)
+
+
 def timeit(fn, iters=10, warmup=2):
+    """Median ms per call. Each event pair brackets one call; when that call
+    is short (< 0.2 ms) the pair brackets max(2, 0.2 ms / t) back-to-back calls
+    instead and the time is divided by their count, so the host's per-call
+    Python/launch latency (~5-10 us, box-dependent) and the idle-clock ramp
+    between isolated calls do not masquerade as kernel time. The one-call
+    median stays in SINGLE["ms"] (emitted as ms_single)."""
     import torch
+
+    def med(reps):
+        ts = []
+        for _ in range(iters):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / reps)
+        ts.sort()
+        return ts[len(ts) // 2]
 
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
-    ts = []
-    for _ in range(iters):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        fn()
-        e1.record()
-        e1.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    ts.sort()
-    return ts[len(ts) // 2]
+    single = med(1)
+    SINGLE["ms"] = single
+    if single >= 0.2:
+        return single
+    return min(single, med(max(2, min(100, int(0.2 / max(single, 1e-4))))))
 
 
 def emit(**kw):
+    single = SINGLE.pop("ms", None)
+    if single is not None and "ms" in kw and single != kw["ms"]:
+        kw["ms_single"] = single
     print(json.dumps(kw), flush=True)
 
 
@@ -188,6 +208,7 @@ def bench_transpose(emit, timeit):
         # the paper's two timing modes for the same kernel (lds_pad)
         reps = 20
         ms = timeit(lambda: transpose_reps(x, reps, out)) / reps
+        SINGLE.pop("ms", None)
         emit(bench="transpose_timing_mode", n=n, mode="loop inside kernel", ms=ms, GBps=2 * n * n * 4 / ms / 1e6)
 
 
