@@ -20,7 +20,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_spmv_ell", "iippppfp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_dia", "iiippppfp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_coo", "iqpppppfip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
-_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "ipppppifp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "iqpppppifp")
 
 
 # ---------------------------------------------------------------- formats
@@ -330,7 +330,7 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
         return y
     if isinstance(a, CSRAligned):
         g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
-        _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+        _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.nnz, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), g, float(beta), s)
     elif isinstance(a, CSR):
         g = 1 if kernel == "scalar" else auto_group(a)

@@ -75,11 +75,14 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
             // one base address per RING rows: every load below is base +
             // a compile-time (non-negative) offset
             const Pair<T>* base = s2 + (r0 + 1) * P + cp - NXP;
+            Pair<T>* dbase = d2 + r0 * P + cp;
+            // row guards against one count (u < rem): row u's prefetch guard
+            // is row u + 1's compute guard, one compare per row, no row index
+            const int rem = re - r0;
 #pragma unroll
             for (int u = 0; u < RING; ++u) {
-                const int r = r0 + u;
-                if (r < re) {
-                    if (r + 1 < re) {  // prefetch row r + 1: its x pairs, and row r + 1 + B into the free slot
+                if (u < rem) {
+                    if (u + 1 < rem) {  // prefetch row r + 1: its x pairs, and row r + 1 + B into the free slot
                         const Pair<T>* rp = base + u * P;  // pair column c0 / 2 - NXP of row r + 1
                         win[(u + 1 + 2 * B) % RING] = rp[B * P + NXP];
 #pragma unroll
@@ -110,8 +113,9 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
                         Pair<T> o;
                         o.v[0] = out[0];
                         o.v[1] = out[1];
-                        d2[r * P + cp] = o;
+                        dbase[u * P] = o;
                     } else {
+                        const int r = r0 + u;
                         if (w0) dst[r * PW + c0] = out[0];
                         if (w1) dst[r * PW + c0 + 1] = out[1];
                     }
@@ -135,7 +139,14 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     constexpr int B = G::B, H = G::H, PW = G::PW, LW = G::LW, LH = G::LH;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* L0 = reinterpret_cast<T*>(smem);
-    T* L1 = L0 + LH * PW;
+    // the second buffer's element offset goes through an opaque SGPR: folded
+    // as a constant, its byte offset (72 KB for fp64 order 8) overflows the
+    // 16-bit ds_read offset field and every LDS read of the unrolled step
+    // loop paid its own v_add_u32 (5 per row pair)
+    // (only where it overflows: a fitting constant offset costs nothing)
+    int l1_off = LH * PW;
+    if constexpr ((size_t)(LH + 3 * B + 3) * PW * sizeof(T) > 65535) asm volatile("" : "+s"(l1_off));
+    T* L1 = L0 + l1_off;
     const int tyi = (int)blockIdx.x / tiles_x;
     const int txi = (int)blockIdx.x - tyi * tiles_x;
     const int ox = g.xb + txi * TX, oy = g.yb + tyi * TY;  // output origin (grid)

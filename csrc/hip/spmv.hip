@@ -303,13 +303,20 @@ CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const floa
     CME_LAUNCH_STATUS();
 }
 
-// Aligned CSR (every rp[i] % 4 == 0, col/val 16-B aligned): group 1..64.
-CME_EXPORT int cme_spmv_csr_aligned(int nrows, const int* rp, const int* col, const float* val, const float* x,
-                                    float* y, int group, float beta, void* stream) {
+// Aligned CSR (every rp[i] % 4 == 0, col/val 16-B aligned): group 1..64;
+// nnz = col/val length (selects the stream loads).
+CME_EXPORT int cme_spmv_csr_aligned(int nrows, long long nnz, const int* rp, const int* col, const float* val,
+                                    const float* x, float* y, int group, float beta, void* stream) {
     hipStream_t s = as_stream(stream);
     if (((uintptr_t)col % 16) || ((uintptr_t)val % 16)) return (int)hipErrorInvalidValue;
-    // CME_SPMV_NT=0/1 selects the stream loads (default: non-temporal)
-    const bool nt = cme::tune_get(cme::kTuneSpmvNT) != 0;
+    // CME_SPMV_NT: 0 plain stream loads, 1 non-temporal, 2 (default) non-temporal
+    // only when the col/val stream cannot stay in the 256 MB Infinity Cache
+    // between calls. Measured (profiles/spmv_nt_r4.md): non-temporal wins cold
+    // (5pt-16M 211 vs 219 us, random-1M 104 vs 111) but loses whenever the
+    // stream is cache-resident across calls (27pt-1M warm 50 vs 40 us, skew-1M
+    // 1.50 vs 1.26 ms, every column-blocked case).
+    const int mode = cme::tune_get(cme::kTuneSpmvNT);
+    const bool nt = mode == 2 ? nnz * 8 > (256ll << 20) : mode != 0;
     switch (group) {
 #define V(G)                                                                                                      \
     case G:                                                                                                       \

@@ -30,7 +30,7 @@ enum TuneKey : int {
     kTuneStreamNThinWaves, // CME_STREAMN_THIN_WAVES
     kTuneStreamNCapPct,    // CME_STREAMN_CAPPCT
     kTuneSpmvScanMulti,    // CME_SPMVSCAN_MULTI
-    kTuneSpmvNT,           // CME_SPMV_NT
+    kTuneSpmvNT,           // CME_SPMV_NT: aligned-CSR stream loads (0 plain, 1 non-temporal, 2 by size)
     kTuneSpmvDia1,         // CME_SPMV_DIA1
     kTunePipeTaper,        // CME_PIPE_TAPER: half-height last chunks per strip of a multi-round pass (0 off, -1 auto)
     kTuneCount

@@ -77,6 +77,23 @@ def test_spmv_gpu(gpu, mat, fmt):
     np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.gpu
+def test_spmv_csr_aligned_stream_load_modes_bitwise(gpu):
+    """The aligned-CSR stream-load modes (tuning knob spmv_nt: 0 plain, 1
+    non-temporal, 2 by matrix size) only change cache hints: bitwise equal."""
+    from cme213x.utils import tuning
+
+    a = random_csr(30000, 30000, 16, seed=6)
+    dev = to_csr_aligned(a).to(gpu)
+    x = torch.randn(a.ncols, device=gpu)
+    outs = []
+    for mode in (0, 1, 2):
+        with tuning.override(spmv_nt=mode):
+            outs.append(spmv(dev, x).cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    np.testing.assert_allclose(outs[2].numpy(), _ref(a, x.cpu()), rtol=1e-4, atol=1e-3)
+
+
 def test_colblocked_format_choice_and_blocks():
     """Column-blocked CSR: block count from the x footprint (2 MB per block),
     block-relative columns, and `auto` choosing it only when x exceeds 2 MB
