@@ -144,6 +144,10 @@ _F64_PIPE_MIN_POINTS = 2000 * 2000
 # 4.63 ms FMA / 5.35 exact vs 5.67 / 6.88 for streamN; at 2000^2 the pipelined
 # pass wins (8.5 vs 15.5 ms; profiles/heat_tile_r4.md)
 _F64_TILE_MAX_POINTS = 1200 * 1200
+# ... and fp32 ones too (round 4, benchmarks/bench_small_variants.py, 1000 steps,
+# order 8: 1000^2 tile4 3.69 / tile4_fma 3.33 ms vs pipe3 6.69 / pipe3_fma 5.34;
+# 1500^2 the pipelined pass wins, 5.88 vs 7.94 FMA; profiles/heat_small_r4.md)
+_TILE_MAX_POINTS = _F64_TILE_MAX_POINTS
 
 
 def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool = False) -> int:
@@ -161,12 +165,17 @@ def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool 
     return 3 if fma else 2
 
 
-def auto_kernel(dtype, points: int, tblock: int, solo: bool = False) -> str:
+def auto_kernel(dtype, points: int, tblock: int, solo: bool = False, fast: bool = False, order: int = 8) -> str:
     """Pass kernel for 3-4 step passes: the wave-pipelined pass for fp32 and
     for fp64 subdomains of at least 2000^2 cells (and every fp64 4-step pass:
-    streamN stops at 3 for doubles), streamN below that; a small fp64 grid on
-    one GPU with no neighbours (``solo``) runs the LDS-resident tile pass."""
-    if solo and dtype == torch.float64 and points <= _F64_TILE_MAX_POINTS and tblock >= 2:
+    streamN stops at 3 for doubles), streamN below that; a small grid on one
+    GPU with no neighbours (``solo``) runs the LDS-resident tile pass where it
+    measured faster: order 8 (fp32 and fp64) and fp64 order 4 -- the narrower
+    stencils leave the pipelined pass HBM-light enough to win (fp32 order 2
+    1000^2: pipe4 2.11 vs tile4 2.63 ms FMA; profiles/heat_small_r4.md) --
+    and never in the reassociated arithmetic (``fast``: pipelined only)."""
+    tile_order = order == 8 or (order == 4 and dtype == torch.float64)
+    if solo and not fast and tile_order and points <= _TILE_MAX_POINTS and tblock >= 2:
         return "tile"
     if tblock < 3:
         return "streamn"
@@ -265,7 +274,8 @@ class DistHeat:
             if tblock == "auto":
                 tblock = auto_tblock(dtype, pts, fma, torch.device(device).type, solo)
             if kernel == "auto":
-                kernel = auto_kernel(dtype, pts, tblock, solo and torch.device(device).type == "cuda")
+                kernel = auto_kernel(dtype, pts, tblock, solo and torch.device(device).type == "cuda",
+                                     fast=arith_code(fma) == 2, order=params.order)
         if tblock not in (1, 2, 3, 4):
             raise ValueError("tblock must be 1..4")
         if kernel not in ("streamn", "pipe", "tile"):

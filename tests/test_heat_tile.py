@@ -67,27 +67,42 @@ def test_tile_variants_refuse_single_step_api():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("fma", [False, True])
-def test_hw5_default_path_uses_tile_pass(gpu, fma):
-    """The hw5 driver's automatic choice on a small single-grid fp64 run is the
-    tile pass (four steps per pass), bitwise equal to the CPU oracle's single
-    steps (exact or FMA) -- the reference's 1000^2 shape, 13 steps (three
-    passes and a one-step tail)."""
+def test_hw5_default_path_uses_tile_pass(gpu, fma, dtype):
+    """The hw5 driver's automatic choice on a small single-grid run (fp64, and
+    fp32 since round 4) is the tile pass (four steps per pass), bitwise equal
+    to the CPU oracle's single steps (exact or FMA) -- the reference's 1000^2
+    shape, 13 steps (three passes and a one-step tail)."""
     from cme213x.models.heat2d_dist import DistHeat
 
     p = SimParams(nx=1000, ny=1000, order=8, iters=13, ic=3.0, bc=(0.0, 10.0, 0.0, 10.0), flavor="hw5")
-    sim = DistHeat(p, None, torch.float64, gpu, tblock="auto", kernel="auto", fma=fma)
+    sim = DistHeat(p, None, dtype, gpu, tblock="auto", kernel="auto", fma=fma)
     assert sim.kernel == "tile" and sim.tblock == 4 and sim.solo()
-    ref = DistHeat(p, None, torch.float64, "cpu", variant="naive", fma=fma)
+    ref = DistHeat(p, None, dtype, "cpu", variant="naive", fma=fma)
     for d in (sim, ref):
         (s,) = d.subs.values()
         g, H = s.grid, s.grid.H
         yy, xx = np.meshgrid(np.arange(1000), np.arange(1000), indexing="ij")
-        g.buf[:, H:H + 1000, H:H + 1000] = torch.from_numpy(np.sin(0.01 * xx) * np.cos(0.02 * yy) + 3.0).to(g.device)
+        g.buf[:, H:H + 1000, H:H + 1000] = torch.from_numpy(np.sin(0.01 * xx) * np.cos(0.02 * yy) + 3.0).to(
+            device=g.device, dtype=dtype)
     sim.run(13)
     ref.run(13)
     torch.cuda.synchronize()
     assert np.array_equal(sim.gather_global(), ref.gather_global())
+
+
+def test_auto_kernel_small_grids_pick_tile_except_fast():
+    from cme213x.models.heat2d_dist import auto_kernel
+
+    for dt in (torch.float32, torch.float64):
+        assert auto_kernel(dt, 1000 * 1000, 4, solo=True) == "tile"
+        assert auto_kernel(dt, 2000 * 2000, 4, solo=True) == "pipe"
+        assert auto_kernel(dt, 1000 * 1000, 4, solo=False) == "pipe"
+    assert auto_kernel(torch.float32, 1000 * 1000, 4, solo=True, fast=True) == "pipe"
+    assert auto_kernel(torch.float64, 1000 * 1000, 4, solo=True, order=4) == "tile"
+    for dt, o in ((torch.float32, 4), (torch.float32, 2), (torch.float64, 2)):
+        assert auto_kernel(dt, 1000 * 1000, 4, solo=True, order=o) == "pipe"
 
 
 def test_tile_kernel_only_for_single_grids():
