@@ -54,6 +54,7 @@ __device__ __forceinline__ uint32_t rx_key_out(uint32_t u, int mode) {
     return u;
 }
 
+template <int UNR>
 __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint32_t* __restrict__ keys, long long n,
                                                                      long long chunk, int shift, int nblocks,
                                                                      uint32_t* __restrict__ counts, int mode) {
@@ -79,8 +80,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
     };
     // UNR 16-B loads in flight per lane before their LDS atomics (one load at
     // a time left the kernel waiting on HBM latency: wait-any 0.85 of its
-    // cycles, profiles/sort_r3.md)
-    constexpr int UNR = 4;
+    // cycles, profiles/sort_r3.md); tuning knob radix_up_unr
     constexpr long long STEP = (long long)kSortThreads * 4;
     long long i = b0 + threadIdx.x * 4;
     if (vec) {
@@ -748,6 +748,7 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     uint32_t* counts = (uint32_t*)ws;
     uint32_t* totals = counts + (size_t)nb * kBins;
     const int npass = (bit1 - bit0 + kRadixBits - 1) / kRadixBits;
+    const int up_unr = (int)cme::tune_get(cme::kTuneRadixUpUnr);  // upsweep 16-B loads in flight per lane: 4, 8, 16
     const uint32_t* ki = in;
     const uint32_t* vi = vin;
     for (int p = 0; p < npass; ++p) {
@@ -756,8 +757,18 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         uint32_t* vo = vin ? (to_out ? vout : vtmp) : nullptr;
         const int shift = bit0 + kRadixBits * p;
         const int mi = p == 0 ? mode : 0, mo = p == npass - 1 ? mode : 0;
-        hipLaunchKernelGGL(radix_upsweep_kernel, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb, counts,
-                           mi);
+        switch (up_unr) {
+#define CME_UP(U)                                                                                                  \
+    case U:                                                                                                       \
+        hipLaunchKernelGGL(radix_upsweep_kernel<U>, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift, nb,     \
+                           counts, mi);                                                                           \
+        break;
+            CME_UP(8) CME_UP(16)
+#undef CME_UP
+            default:
+                hipLaunchKernelGGL(radix_upsweep_kernel<4>, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift,
+                                   nb, counts, mi);
+        }
         hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins), dim3(1024), 0, s, counts, nb, totals);
 #define CME_DS(V, A, P)                                                                                           \
     do {                                                                                                          \
@@ -859,7 +870,7 @@ CME_EXPORT int cme_merge_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel);
+CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel<4>);
 CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
 CME_REGISTER_KERNEL(ms_block_sort, 512, ms_block_sort_kernel<false>);
 CME_REGISTER_KERNEL(ms_merge_pass, 256, ms_merge_pass_kernel<false>);

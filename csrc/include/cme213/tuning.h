@@ -33,6 +33,7 @@ enum TuneKey : int {
     kTuneSpmvNT,           // CME_SPMV_NT: aligned-CSR stream loads (0 plain, 1 non-temporal, 2 by size)
     kTuneSpmvDia1,         // CME_SPMV_DIA1
     kTunePipeTaper,        // CME_PIPE_TAPER: half-height last chunks per strip of a multi-round pass (0 off, -1 auto)
+    kTuneRadixUpUnr,       // CME_RADIX_UP_UNR: radix upsweep 16-B loads in flight per lane (4, 8, 16)
     kTuneCount
 };
 
