@@ -148,17 +148,27 @@ _F64_TILE_MAX_POINTS = 1200 * 1200
 # order 8: 1000^2 tile4 3.69 / tile4_fma 3.33 ms vs pipe3 6.69 / pipe3_fma 5.34;
 # 1500^2 the pipelined pass wins, 5.88 vs 7.94 FMA; profiles/heat_small_r4.md)
 _TILE_MAX_POINTS = _F64_TILE_MAX_POINTS
+# solo fp32 order-8 grids above the tile range and up to this size: 3-step passes (auto_tblock)
+_F32_PIPE3_MAX_POINTS = 2500 * 2500
 
 
-def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool = False) -> int:
+def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool = False, order: int = 8) -> int:
     """Timesteps per HBM pass (and per halo exchange) for a subdomain of
     ``points`` cells: 4 for fp32 (pipelined pass, every N of the 16384^2
     bench) and for large fp64 subdomains; 3 (FMA) or 2 (exact) for small fp64
     ones, where streamN wins (exact fp64 1000^2: stream2 0.0073 vs stream3
-    0.0087 ms/iter). On the CPU backend: 1 (no temporal blocking)."""
+    0.0087 ms/iter). A solo fp32 order-8 grid between the tile pass's range
+    and 2500^2 takes 3 (exact / FMA; the 4-step pass's warm-up rows dominate
+    there: 2000^2 pipe3 3.99 vs pipe4 4.97 ms per 400 steps; the reassociated
+    arithmetic keeps 4, 3.97 vs 3.49; profiles/heat_small_r4.md). On the CPU
+    backend: 1 (no temporal blocking)."""
     if torch.device(device).type != "cuda":
         return 1
-    if dtype == torch.float32 or points >= _F64_PIPE_MIN_POINTS:
+    if dtype == torch.float32:
+        if solo and order == 8 and arith_code(fma) != 2 and _TILE_MAX_POINTS < points <= _F32_PIPE3_MAX_POINTS:
+            return 3
+        return 4
+    if points >= _F64_PIPE_MIN_POINTS:
         return 4
     if solo and points <= _F64_TILE_MAX_POINTS:
         return 4  # the tile pass (auto_kernel)
@@ -272,7 +282,7 @@ class DistHeat:
                                             for r in range(self.world)))
             solo = self.world == 1 and not any(self.periodic)
             if tblock == "auto":
-                tblock = auto_tblock(dtype, pts, fma, torch.device(device).type, solo)
+                tblock = auto_tblock(dtype, pts, fma, torch.device(device).type, solo, order=params.order)
             if kernel == "auto":
                 kernel = auto_kernel(dtype, pts, tblock, solo and torch.device(device).type == "cuda",
                                      fast=arith_code(fma) == 2, order=params.order)

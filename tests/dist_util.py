@@ -17,6 +17,27 @@ def free_port() -> int:
     return p
 
 
+def init_single_rank(backend: str = "nccl") -> None:
+    """World-1 process group on cuda:0 (no-op if one exists). A port that
+    free_port() saw free can be taken again before the store binds it
+    (EADDRINUSE); the rendezvous then fails before any GPU work, so another
+    port is tried."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return
+    for attempt in range(5):
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        try:
+            dist.init_process_group(backend, rank=0, world_size=1, device_id=torch.device("cuda", 0))
+            return
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
+
+
 def _worker(rank, world, port, fn, args, q):
     try:
         if REPO not in sys.path:

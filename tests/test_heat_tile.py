@@ -105,6 +105,20 @@ def test_auto_kernel_small_grids_pick_tile_except_fast():
         assert auto_kernel(dt, 1000 * 1000, 4, solo=True, order=o) == "pipe"
 
 
+def test_auto_tblock_fp32_order8_mid_sizes_take_three_steps():
+    from cme213x.models.heat2d_dist import auto_tblock
+
+    f32 = torch.float32
+    assert auto_tblock(f32, 2000 * 2000, False, "cuda", True) == 3
+    assert auto_tblock(f32, 2000 * 2000, True, "cuda", True) == 3
+    assert auto_tblock(f32, 2000 * 2000, "fast", "cuda", True) == 4
+    assert auto_tblock(f32, 2000 * 2000, False, "cuda", True, order=4) == 4
+    assert auto_tblock(f32, 2000 * 2000, False, "cuda", False) == 4  # distributed: halo cadence unchanged
+    assert auto_tblock(f32, 3000 * 3000, False, "cuda", True) == 4
+    assert auto_tblock(f32, 1000 * 1000, False, "cuda", True) == 4  # the tile pass
+    assert auto_tblock(f32, 2000 * 2000, False, "cpu", True) == 1
+
+
 def test_tile_kernel_only_for_single_grids():
     from cme213x.models.heat2d_dist import DistHeat
 

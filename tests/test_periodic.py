@@ -177,9 +177,9 @@ def _auto_rank(rank, world):
     orig = hd.auto_tblock
     seen = []
 
-    def probe(dtype, points, fma, device="cuda", solo=False):  # decide as on the GPU
+    def probe(dtype, points, fma, device="cuda", solo=False, **kw):  # decide as on the GPU
         seen.append(points)
-        return orig(dtype, points, fma, "cuda", solo)
+        return orig(dtype, points, fma, "cuda", solo, **kw)
 
     hd.auto_tblock = probe
     hd._F64_PIPE_MIN_POINTS = 50 * 50  # 99^2 on 4 ranks: 50x50 and 49x50 blocks straddle it

@@ -20,16 +20,13 @@ import numpy as np
 import pytest
 import torch
 
-from dist_util import REPO, free_port, run_ranks
+from dist_util import REPO, free_port, init_single_rank, run_ranks
 
 
 def _setup_single():
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
-                      LOCAL_RANK="0")
-    if not dist.is_initialized():
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    init_single_rank("nccl")
 
 
 def _params(method, iters=9):
