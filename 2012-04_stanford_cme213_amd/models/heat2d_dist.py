@@ -167,6 +167,8 @@ def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool 
     if dtype == torch.float32:
         if solo and order == 8 and arith_code(fma) != 2 and _TILE_MAX_POINTS < points <= _F32_PIPE3_MAX_POINTS:
             return 3
+        if solo and order == 2:  # HBM-bound: 5-6 steps per pass (pipe5 / pipe6; heat_small_r4.md)
+            return 6 if arith_code(fma) == 1 else 5
         return 4
     if points >= _F64_PIPE_MIN_POINTS:
         return 4
@@ -273,6 +275,7 @@ class DistHeat:
         # ("auto": fall back to the Python loop if it fails; "on": raise)
         self.native_mode = native
         self.native_info: dict | None = None
+        auto_tb = tblock == "auto"
         if tblock == "auto" or kernel == "auto":
             # by the LARGEST subdomain of the whole decomposition -- the same
             # answer on every rank (an uneven split must not give neighbours
@@ -286,8 +289,12 @@ class DistHeat:
             if kernel == "auto":
                 kernel = auto_kernel(dtype, pts, tblock, solo and torch.device(device).type == "cuda",
                                      fast=arith_code(fma) == 2, order=params.order)
-        if tblock not in (1, 2, 3, 4):
-            raise ValueError("tblock must be 1..4")
+        deep = (dtype == torch.float32 and torch.device(device).type == "cuda" and self.world == 1
+                and not any(self.periodic) and kernel == "pipe")
+        if auto_tb and tblock > 4 and not deep:
+            tblock = 4  # an explicitly chosen kernel other than the pipelined pass
+        if tblock not in ((1, 2, 3, 4, 5, 6) if deep else (1, 2, 3, 4)):
+            raise ValueError("tblock must be 1..4 (5-6: solo fp32 GPU grids, kernel='pipe')")
         if kernel not in ("streamn", "pipe", "tile"):
             raise ValueError("kernel must be 'streamn', 'pipe' or 'tile'")
         if kernel == "tile" and (self.world != 1 or any(self.periodic)):
@@ -634,6 +641,8 @@ class DistHeat:
 
         from .. import _ext
 
+        if self.tblock > 4:
+            raise ValueError("the native loop runs 1-4 steps per pass (tblock 5-6: solo grids, run())")
         if rccl is not None and len(self.subs) != 1:
             raise ValueError("RCCL transport: one subdomain per process")
         if rccl is not None and ipc is not None:

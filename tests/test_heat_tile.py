@@ -119,6 +119,49 @@ def test_auto_tblock_fp32_order8_mid_sizes_take_three_steps():
     assert auto_tblock(f32, 2000 * 2000, False, "cpu", True) == 1
 
 
+def test_deep_passes_only_for_solo_fp32_gpu_pipe():
+    from cme213x.models.heat2d_dist import DistHeat, auto_tblock
+
+    f32 = torch.float32
+    assert auto_tblock(f32, 4096 * 4096, False, "cuda", True, order=2) == 5
+    assert auto_tblock(f32, 4096 * 4096, True, "cuda", True, order=2) == 6
+    assert auto_tblock(f32, 4096 * 4096, True, "cuda", False, order=2) == 4
+    p = SimParams(nx=100, ny=100, order=2, iters=2, flavor="hw5")
+    for kw in ({"local_ranks": [0, 1], "world": 2}, {"periodic": (True, False)}):
+        with pytest.raises(ValueError, match="tblock"):
+            DistHeat(p, None, f32, "cpu", tblock=6, kernel="pipe", **kw)
+    with pytest.raises(ValueError, match="tblock"):
+        DistHeat(p, None, torch.float64, "cpu", tblock=5, kernel="pipe")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fma", [False, True])
+def test_solo_fp32_order2_deep_passes_gpu(gpu, fma):
+    """The automatic choice for a solo fp32 order-2 grid is 5 (exact) or 6
+    (FMA) steps per pipelined pass; bitwise equal to the CPU oracle's single
+    steps over 13 steps (two deep passes and a tail); the native loop refuses
+    such a depth."""
+    from cme213x.models.heat2d_dist import DistHeat
+
+    n = 700
+    p = SimParams(nx=n, ny=n, order=2, iters=13, ic=3.0, bc=(0.0, 10.0, 0.0, 10.0), flavor="hw5")
+    sim = DistHeat(p, None, torch.float32, gpu, tblock="auto", kernel="auto", fma=fma)
+    assert sim.kernel == "pipe" and sim.tblock == (6 if fma else 5) and sim.solo()
+    ref = DistHeat(p, None, torch.float32, "cpu", variant="naive", fma=fma)
+    for d in (sim, ref):
+        (s,) = d.subs.values()
+        g, H = s.grid, s.grid.H
+        yy, xx = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        g.buf[:, H:H + n, H:H + n] = torch.from_numpy(np.sin(0.01 * xx) * np.cos(0.02 * yy) + 3.0).to(
+            device=g.device, dtype=torch.float32)
+    sim.run(13)
+    ref.run(13)
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
+    with pytest.raises(ValueError, match="native loop"):
+        sim.run_native(4, transport=2)
+
+
 def test_tile_kernel_only_for_single_grids():
     from cme213x.models.heat2d_dist import DistHeat
 
