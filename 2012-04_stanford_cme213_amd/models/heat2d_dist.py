@@ -172,8 +172,11 @@ def auto_tblock(dtype, points: int, fma: bool, device: str = "cuda", solo: bool 
         return 4
     if points >= _F64_PIPE_MIN_POINTS:
         return 4
-    if solo and points <= _F64_TILE_MAX_POINTS:
-        return 4  # the tile pass (auto_kernel)
+    if solo and (points <= _F64_TILE_MAX_POINTS or order < 8):
+        # the tile pass (auto_kernel) / orders 2 and 4: the pipelined 4-step
+        # pass (1500^2 order 2: pipe4 1.42 vs stream2 2.25 ms per 400 steps
+        # exact, 1.29 vs stream3 1.64 FMA; heat_small_r4.md)
+        return 4
     return 3 if fma else 2
 
 

@@ -117,6 +117,12 @@ def test_auto_tblock_fp32_order8_mid_sizes_take_three_steps():
     assert auto_tblock(f32, 3000 * 3000, False, "cuda", True) == 4
     assert auto_tblock(f32, 1000 * 1000, False, "cuda", True) == 4  # the tile pass
     assert auto_tblock(f32, 2000 * 2000, False, "cpu", True) == 1
+    f64 = torch.float64
+    for o in (2, 4):  # fp64 low orders between the tile range and 2000^2: the pipelined 4-step pass
+        assert auto_tblock(f64, 1500 * 1500, False, "cuda", True, order=o) == 4
+    assert auto_tblock(f64, 1500 * 1500, False, "cuda", True, order=8) == 2
+    assert auto_tblock(f64, 1500 * 1500, True, "cuda", True, order=8) == 3
+    assert auto_tblock(f64, 1500 * 1500, False, "cuda", False, order=2) == 2
 
 
 def test_deep_passes_only_for_solo_fp32_gpu_pipe():
@@ -160,6 +166,30 @@ def test_solo_fp32_order2_deep_passes_gpu(gpu, fma):
     assert np.array_equal(sim.gather_global(), ref.gather_global())
     with pytest.raises(ValueError, match="native loop"):
         sim.run_native(4, transport=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [2, 4])
+def test_solo_fp64_low_order_mid_size_pipe4_gpu(gpu, order):
+    """fp64 order 2 / 4 grids between the tile range and 2000^2 (solo): the
+    automatic choice is the pipelined 4-step pass, bitwise equal to the CPU
+    oracle (exact arithmetic, 9 steps: two passes and a tail)."""
+    from cme213x.models.heat2d_dist import DistHeat
+
+    n = 1250
+    p = SimParams(nx=n, ny=n, order=order, iters=9, ic=3.0, bc=(0.0, 10.0, 0.0, 10.0), flavor="hw5")
+    sim = DistHeat(p, None, torch.float64, gpu, tblock="auto", kernel="auto")
+    assert sim.kernel == "pipe" and sim.tblock == 4 and sim.solo()
+    ref = DistHeat(p, None, torch.float64, "cpu", variant="naive")
+    for d in (sim, ref):
+        (s,) = d.subs.values()
+        g, H = s.grid, s.grid.H
+        yy, xx = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        g.buf[:, H:H + n, H:H + n] = torch.from_numpy(np.sin(0.01 * xx) * np.cos(0.02 * yy) + 3.0).to(g.device)
+    sim.run(9)
+    ref.run(9)
+    torch.cuda.synchronize()
+    assert np.array_equal(sim.gather_global(), ref.gather_global())
 
 
 def test_tile_kernel_only_for_single_grids():
