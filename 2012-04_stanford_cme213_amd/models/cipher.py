@@ -32,6 +32,7 @@ def run_hw1_cipher(path: str, replicate: int = 16, shift: int | None = None, dev
     data = np.tile(text, replicate)
     host = torch.from_numpy(data)
     res = {"bytes": int(data.size), "shift": shift, "variants": {}}
+    shift_cipher(host[:4096], shift)  # CPU warm-up (OpenMP thread start-up, library load)
     if device == "cpu":
         t = EventTimer("host shift cypher")
         with t:

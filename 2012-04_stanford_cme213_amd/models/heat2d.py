@@ -172,6 +172,11 @@ def run_hw2(params_path: str, dtype=torch.float32, device: str | None = None, ou
         cpu_grid = HeatGrid(p, dtype, "cpu")
         if write_files:
             cpu_grid.save_text("init")
+        # warm-up of the CPU oracle, as the GPU variants get below: the first
+        # call pays the OpenMP runtime's thread start-up and the library load
+        # (580 ms vs 0.3 ms warm at 200^2 x 10), which would
+        # inflate every GPU-over-CPU speed-up on small grids
+        HeatGrid(p, dtype, "cpu").run(1, "naive")
         t = EventTimer(f"cpu computation {tname}")
         with t:
             cpu_grid.run(p.iters, "naive")

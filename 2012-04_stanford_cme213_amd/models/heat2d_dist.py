@@ -310,6 +310,10 @@ class DistHeat:
         if self.arith == 2 and tblock > 1 and (dtype != torch.float32 or params.order != 8 or kernel == "tile"
                                                or (kernel != "pipe" and torch.device(device).type == "cuda")):
             raise ValueError("fma='fast' multi-step passes: fp32, order 8, kernel='pipe'")
+        if self.arith == 2 and tblock > 4:
+            # the reassociated pass exists for 2-4 steps (heat_fast.hip); say so
+            # here rather than fail on a missing variant in run()
+            raise ValueError("fma='fast' runs 1-4 steps per pass (tblock <= 4)")
         self.fma = self.arith == 1
         # 3-4 step passes: streamN (one wave holds every step) or the
         # wave-pipelined kernel (csrc/hip/heat_pipe.hip); identical results
@@ -741,33 +745,25 @@ class DistHeat:
             self.comm.allreduce_(t, "min")
             return bool(t.item() == 1.0)
 
-        try:
-            _ext.hip()
-            ok = True
-        except Exception as e:  # noqa: BLE001 - reported; every rank falls back together
-            print(f"DistHeat rank {self.comm.rank}: native library unavailable ({e})", flush=True)
-            ok = False
-        handle, kind = None, "loopback"
+        kind = "loopback"
         # RCCL may be asked for at world 1 too (a periodic grid's halos are
         # then self-sends); IPC needs other processes to map
-        if agree(ok) and (self.comm.size > 1 or transport == "rccl"):
+        need_transport = self.comm.size > 1 or transport == "rccl"
+        if need_transport:
             backend = getattr(self.comm, "backend", None)
             kind = transport or ("rccl" if backend == "nccl" else "ipc")
-            try:
-                if kind == "rccl":
-                    from ..parallel.rccl import NativeRccl
 
-                    handle = NativeRccl(getattr(self.comm, "group", None))
-                else:
-                    from ..parallel.ipc import NativeIpc
+        def open_transport():
+            if kind == "rccl":
+                from ..parallel.rccl import NativeRccl
 
-                    handle = NativeIpc(getattr(self.comm, "group", None))
-            except Exception as e:  # noqa: BLE001
-                print(f"DistHeat rank {self.comm.rank}: native {kind} transport unavailable ({e})", flush=True)
-                ok = False
-            ok = agree(ok)
-        elif not ok:
-            ok = False
+                return NativeRccl(getattr(self.comm, "group", None))
+            from ..parallel.ipc import NativeIpc
+
+            return NativeIpc(getattr(self.comm, "group", None))
+
+        ok, handle = native_setup_agreement(agree, _ext.hip, open_transport if need_transport else None,
+                                            f"DistHeat rank {self.comm.rank}", kind)
         if ok:
             ok = False
             for f in ((True, False) if fused else (False,)):
@@ -956,6 +952,33 @@ class DistHeat:
             b, st = s.blk, s.grid.state()
             out[B + b.y0:B + b.y0 + b.ny, B + b.x0:B + b.x0 + b.nx] = st[B:B + b.ny, B:B + b.nx]
         return out
+
+
+def native_setup_agreement(agree, load_lib, open_transport, who: str = "", kind: str = "") -> tuple[bool, object]:
+    """The collective first half of :meth:`DistHeat.enable_native`: load the
+    native library, then (``open_transport`` not None) open the transport,
+    each step followed by ``agree`` (an all-rank AND). Every rank makes the
+    same number of ``agree`` calls and returns the same ``ok`` -- a rank whose
+    library loaded falls back with a peer whose library did not, instead of
+    entering the self-test's collectives alone. Returns
+    ``(ok, handle)``; the handle of a transport opened on a rank whose peer
+    failed is returned too, so the caller can abort it."""
+    try:
+        load_lib()
+        ok = True
+    except Exception as e:  # noqa: BLE001 - reported; every rank falls back together
+        print(f"{who}: native library unavailable ({e})", flush=True)
+        ok = False
+    ok = agree(ok)
+    handle = None
+    if ok and open_transport is not None:
+        try:
+            handle = open_transport()
+        except Exception as e:  # noqa: BLE001
+            print(f"{who}: native {kind} transport unavailable ({e})", flush=True)
+            ok = False
+        ok = agree(ok)
+    return ok, handle
 
 
 def native_selftest(sim: "DistHeat", kind: str, handle, fused: bool, n: int = 1024) -> bool:

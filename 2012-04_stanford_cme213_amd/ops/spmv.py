@@ -21,6 +21,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_spmv_dia", "iiippppfp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_coo", "iqpppppfip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "iqpppppifp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_stream", "ipppppifp")
 
 
 # ---------------------------------------------------------------- formats
@@ -310,10 +311,25 @@ def auto_group(a: CSR) -> int:
     return g
 
 
+def stream_rows(a: CSR) -> int:
+    """Rows per workgroup of the CSR-stream kernel: 256 / 128 / 64 for a mean
+    row length up to 8 / 16 / beyond, so a block's nonzeros (R x mean) stay
+    well inside its 4096-product LDS buffer (a heavier block still runs, on
+    the kernel's wave-per-row fallback)."""
+    mean = a.nnz / max(1, a.nrows)
+    return 256 if mean <= 8 else (128 if mean <= 16 else 64)
+
+
+# mean row length below which CSR "auto" takes the stream kernel
+STREAM_MAX_MEAN = 16
+
+
 def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
     """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
-    "scalar", "vector", or "auto" (vector with auto group). To pick the
-    FORMAT by the matrix structure, convert once with :func:`prepare`."""
+    "scalar", "vector", "stream" (CSR-stream: row blocks staged through LDS),
+    or "auto" (stream for a mean row length below 16, where CSR-vector idles
+    most of its lanes; vector with auto group above). To pick the FORMAT by
+    the matrix structure, convert once with :func:`prepare`."""
     if y is None:
         nrows = a.ell.nrows if isinstance(a, HYB) else a.nrows
         y = torch.zeros(nrows, dtype=torch.float32, device=x.device)
@@ -332,6 +348,10 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
         g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
         _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.nnz, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), g, float(beta), s)
+    elif isinstance(a, CSR) and (kernel == "stream" or
+                                 (kernel == "auto" and a.nnz < STREAM_MAX_MEAN * max(1, a.nrows))):
+        _ext.call_hip("cme_spmv_csr_stream", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), stream_rows(a), float(beta), s)
     elif isinstance(a, CSR):
         g = 1 if kernel == "scalar" else auto_group(a)
         _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
@@ -433,7 +453,8 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
         parts = fmt.split("_")[2:]
         m = to_csr_colblocked(a, int(parts[0]) << 10, aligned=not (len(parts) > 1 and parts[1] == "u"))
         return fmt, (m.to(device) if device is not None else m)
-    conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_aligned": to_csr_aligned,
+    conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_stream": lambda m: m,
+            "csr_aligned": to_csr_aligned,
             "csr_cb": to_csr_colblocked,
             "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}
     if fmt not in conv:

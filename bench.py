@@ -72,6 +72,127 @@ def selftest(comm, dev, args) -> bool:
     return bool(torch.equal(va, vb))
 
 
+HBM_PEAK_GBPS = 8000.0  # MI355X nominal
+
+
+def bench_primitives(dev) -> dict:
+    """BASELINE.json configs #2-#4 on this rank's GPU, each behind an oracle
+    check (``*_ok``): the 8192^2 fp32 LDS-tiled transpose (production ``vec``
+    and the padded 32x32 ``lds_pad`` of the lecture ladder; ``torch.equal``
+    against ``x.t()``; my-refs/MatrixTranspose.pdf p.19), the 2^26 fp32 scan
+    (decoupled look-back and Blelloch) and reduction against a float64 torch
+    reference (my-refs/scan.pdf p.16 Table 2), and SpMV on the 1M-row 5-point
+    Laplacian in CSR (``auto``: the CSR-stream kernel) and ELL with the
+    256 MB Infinity Cache defeated (operand copies >= 768 MB visited
+    round-robin; refs/Bell SC 2009.pdf §4.2), against a float64 reference.
+    Each figure is the median of event-timed batches of back-to-back calls
+    (hipGraph replays for SpMV). Effective GB/s counts the bytes the
+    algorithm must move (transpose and scan: read + write; reduction: read)."""
+    import torch
+
+    from cme213x.ops import scan as sc
+    from cme213x.ops.spmv import laplacian, prepare, spmv
+    from cme213x.ops.transpose import transpose
+
+    out = {}
+
+    def med_ms(fn, calls, reps=7):
+        fn()
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(calls):
+                fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / calls)
+        return sorted(ts)[reps // 2]
+
+    # config #2: transpose 8192^2 fp32
+    n = 8192
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.rand(n, n, device=dev, generator=g)
+    y = torch.empty_like(x)
+    ref_t = x.t().contiguous()
+    for v in ("vec", "lds_pad"):
+        transpose(x, v, y)
+        ok = bool(torch.equal(y, ref_t))
+        ms = med_ms(lambda: transpose(x, v, y), 20)
+        gbps = 2 * n * n * 4 / ms / 1e6
+        out[f"transpose_{v}_ms"] = round(ms, 4)
+        out[f"transpose_{v}_GBps"] = round(gbps, 1)
+        out[f"transpose_{v}_pct_peak"] = round(100 * gbps / HBM_PEAK_GBPS, 1)
+        out[f"transpose_{v}_ok"] = ok
+    del x, y, ref_t
+
+    # config #3: 2^26 scan + reduction, fp32. Bernoulli(0.2) values: every
+    # partial sum is an integer below 2^24 (the total is ~1.34e7), exact in
+    # fp32 in any association order -- so the check is bitwise against the
+    # float64 prefix sums, whatever tree the kernel uses
+    n = 1 << 26
+    x = (torch.rand(n, device=dev, generator=g) < 0.2).float()
+    y = torch.empty_like(x)
+    ref = torch.cumsum(x.double(), 0)
+    assert float(ref[-1]) < 2 ** 24
+    ref32 = ref.float()
+    for algo in ("lookback", "blelloch"):
+        sc.scan(x, False, y, algo)
+        ok = bool(torch.equal(y, ref32))
+        ms = med_ms(lambda: sc.scan(x, False, y, algo), 20)
+        out[f"scan_{algo}_ms"] = round(ms, 4)
+        out[f"scan_{algo}_GBps"] = round(8 * n / ms / 1e6, 1)
+        out[f"scan_{algo}_pct_peak"] = round(100 * 8 * n / ms / 1e6 / HBM_PEAK_GBPS, 1)
+        out[f"scan_{algo}_ok"] = ok
+    r = sc.reduce(x, "sum", "vector")
+    ok = float(r) == float(ref[-1])
+    ms = med_ms(lambda: sc.reduce(x, "sum", "vector"), 20)
+    out["reduce_ms"] = round(ms, 4)
+    out["reduce_GBps"] = round(4 * n / ms / 1e6, 1)
+    out["reduce_ok"] = ok
+    del x, y, ref, ref32
+
+    # config #4: 1M x 1M 5-point Laplacian, CSR / ELL, Infinity Cache defeated
+    A = laplacian("5pt", 1000)
+    xh = torch.rand(A.ncols, generator=torch.Generator().manual_seed(3))
+    rows = torch.repeat_interleave(torch.arange(A.nrows), torch.diff(A.rp.long()))
+    ref = torch.zeros(A.nrows, dtype=torch.float64).index_add_(0, rows, A.val.double() * xh.double()[A.col.long()])
+    for fmt in ("csr", "ell"):
+        _, m = prepare(A, fmt, dev)
+        yy = spmv(m, xh.to(dev))
+        ok = bool(torch.allclose(yy.cpu().double(), ref, rtol=1e-5, atol=1e-5))
+        nbytes = sum(t.numel() * t.element_size() for t in vars(m).values() if isinstance(t, torch.Tensor))
+        nbytes += 4 * (A.ncols + A.nrows)
+        sets = []
+        for _ in range(max(1, -(-(768 << 20) // nbytes))):
+            mm = type(m)(**{k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in vars(m).items()})
+            sets.append((mm, xh.to(dev), torch.empty(A.nrows, device=dev)))
+        calls = 2 * len(sets)
+
+        def cold():
+            for i in range(calls):
+                mm, xx, yo = sets[i % len(sets)]
+                spmv(mm, xx, yo)
+
+        cold()
+        torch.cuda.synchronize(dev)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            cold()
+        ms = med_ms(gr.replay, 1, reps=5) / calls
+        out[f"spmv_{fmt}_ms"] = round(ms, 5)
+        out[f"spmv_{fmt}_GFLOPs"] = round(2 * A.nnz / ms / 1e6, 1)
+        out[f"spmv_{fmt}_GBps"] = round(nbytes / ms / 1e6, 1)
+        out[f"spmv_{fmt}_ok"] = ok
+        del gr, sets
+    torch.cuda.empty_cache()
+    out["primitives_data"] = ("synthetic, seeded: transpose uniform(0,1); scan / reduce Bernoulli(0.2) fp32 (exact "
+                              "prefixes, bitwise check); SpMV 5-pt Laplacian of a 1000^2 grid, x uniform(0,1), "
+                              "operands >= 768 MB visited round-robin (Infinity Cache defeated)")
+    return out
+
+
 def auto_tblock(points_per_rank: int, kernel: str = "pipe") -> int:
     """Timesteps per pass for a subdomain size and pass kernel.
 
@@ -102,11 +223,12 @@ def main() -> int:
     ap.add_argument("--fma", type=int, choices=[0, 1], default=None,
                     help="1 = --arith fma, 0 = --arith exact")
     ap.add_argument("--arith", choices=["fma", "exact", "fast"], default=None,
-                    help="stencil arithmetic (default fast): fma = FMA-contracted (what nvcc emits for the "
-                         "reference's GPU kernel), exact = no contraction (bitwise = the CPU oracle), fast = "
-                         "reassociated (CFL folded into the weights, symmetric pairs summed first: 17 instead of "
-                         "20 flop-instructions per point; within the reference's 10-ULP criterion of exact, "
-                         "bitwise = the CPU fast oracle); profiles/heat_fast_r4.md has the A/B on one box")
+                    help="stencil arithmetic (default fma): fma = FMA-contracted (what nvcc emits for the "
+                         "reference's GPU kernel; <= 8 ULP of exact after 200 steps on random data), exact = no "
+                         "contraction (bitwise = the CPU oracle), fast = reassociated (CFL folded into the "
+                         "weights, symmetric pairs summed first: 17 instead of 20 flop-instructions per point; "
+                         "bitwise = the CPU fast oracle, but it drifts past the reference's 10-ULP criterion "
+                         "within 10 steps on random data: profiles/heat_arith_ulp_r5.md)")
     ap.add_argument("--tblock", type=int, choices=[0, 1, 2, 3, 4], default=0,
                     help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos); "
                          "0 = by subdomain size (auto_tblock)")
@@ -126,8 +248,12 @@ def main() -> int:
                     help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
                          "(tests; never the reported number)")
     ap.add_argument("--ic", choices=["uniform", "random", "both"], default="both",
-                    help="uniform: the reference's IC 5.0 only (the headline value); both: also time the same K "
-                         "steps from a random-init field (ms_per_step_random)")
+                    help="both (default): time K steps from the reference's uniform IC 5.0 (value_uniform) and from "
+                         "a random-init field (the headline value); uniform: the uniform IC only")
+    ap.add_argument("--no-primitives", dest="primitives", action="store_false",
+                    help="N = 1: skip the BASELINE configs #2-#4 (transpose / scan / SpMV) measured after the stencil")
+    ap.add_argument("--no-arith-compare", dest="arith_compare", action="store_false",
+                    help="N = 1: skip timing the other arithmetic (fma <-> fast) on the same fields")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0 with a gloo control plane and the IPC transport "
                          "(exercises the multi-rank flow on a 1-GPU box; the number is not a scaling result)")
@@ -135,7 +261,7 @@ def main() -> int:
     if args.share_gpu:
         args.transport = "ipc"
     if args.arith is None:
-        args.arith = "fast" if args.fma is None else ("fma" if args.fma else "exact")
+        args.arith = "fma" if args.fma is None else ("fma" if args.fma else "exact")
     args.fma = int(args.arith == "fma")
     # the solver's `fma` argument: False exact, True FMA-contracted, "fast" reassociated
     args.fma_arg = {"exact": False, "fma": True, "fast": "fast"}[args.arith]
@@ -303,6 +429,35 @@ def main() -> int:
         secs_random = timed(args.steps)
         sanity_ok = sanity_ok and sane()
 
+    # N = 1: the other arithmetic on the same two fields with the same
+    # protocol, in the same record: the reassociated pass next to
+    # the FMA-contracted headline (round 4's default; it leaves the 10-ULP
+    # criterion on random data, so it is no longer the headline), or FMA next
+    # to an explicitly chosen fast headline
+    secs_cmp = {}
+    cmp_arith = {"fma": "fast", "fast": "fma"}.get(args.arith)
+    if on_gpu and comm.size == 1 and cmp_arith and args.arith_compare and args.order == 8 and args.kernel == "pipe":
+        sim_f = DistHeat(p, comm, torch.float32, dev, variant=args.variant, tblock=args.tblock,
+                         fma={"fma": True, "fast": "fast"}[cmp_arith], kernel=args.kernel)
+        run_f = sim_f.run
+        fields = {"uniform": init_state}
+        if secs_random is not None:
+            fields["random"] = rand_init
+        for name, st in fields.items():
+            for s in sim_f.subs.values():
+                s.grid.buf.copy_(st[(s.blk.x0, s.blk.y0)])
+            spin_up(run_f)
+            for s in sim_f.subs.values():
+                s.grid.buf.copy_(st[(s.blk.x0, s.blk.y0)])
+            sync()
+            secs_cmp[name] = timed(args.steps, run_f)
+        del sim_f
+        torch.cuda.empty_cache()
+
+    prims = {}
+    if on_gpu and comm.size == 1 and args.primitives:
+        prims = bench_primitives(dev)
+
     if use_native:
         sch = DistHeat.schedule()
         schedule = sch["schedule"] + ("" if sch["probe"] == "not run" else f" (queue probe {sch['probe']})")
@@ -313,6 +468,13 @@ def main() -> int:
     from cme213x.utils import tuning
 
     pipe_vw = tuning.get("pipe_vw") if on_gpu else 0
+    # the headline is the random-init field (BASELINE.json: "synthetic
+    # random-init inputs"); the reference's uniform IC is
+    # value_uniform / ms_per_step_uniform
+    secs_uniform = secs
+    headline_random = secs_random is not None
+    if headline_random:
+        secs = secs_random
     eff = pts * bpp * args.steps / secs / 1e9
     # min HBM traffic: one read + one write of the grid per PASS (a pass
     # advances `tblock` timesteps)
@@ -331,7 +493,8 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": round(eff / BASELINE_GBPS, 2),
             "dtype": "fp32",
-            "data": "synthetic (uniform IC 5.0, Dirichlet BCs 0/10/0/10)",
+            "data": ("synthetic random-init interior, uniform(0, 10), seed 1234 + rank, Dirichlet BCs 0/10/0/10"
+                     if headline_random else "synthetic (uniform IC 5.0, Dirichlet BCs 0/10/0/10)"),
             "config": {
                 "model": f"heat2d-{args.n}x{args.n}-order{args.order} (BASELINE.json config #5)",
                 "global_batch": pts,
@@ -345,8 +508,10 @@ def main() -> int:
                 "lane_columns": ({4: 4, 8: 8}.get(pipe_vw, 8 if args.order == 8 else 4)
                                  if args.kernel == "pipe" and args.tblock >= 3 else 4),
                 "fma": bool(args.fma),
-                "arith": {"fma": "FMA-contracted", "exact": "exact (no contraction)",
-                          "fast": "reassociated (folded CFL weights, pair sums; <= 10 ULP of exact)"}[args.arith],
+                "arith": {"fma": "FMA-contracted (<= 10 ULP of exact: 8 at 4000^2 x 10, 7 at 2048^2 x 200 random)",
+                          "exact": "exact (no contraction)",
+                          "fast": "reassociated (folded CFL weights, pair sums; drifts past 10 ULP of exact on "
+                                  "random data: 15 ULP at 4000^2 x 10 steps, 39 at 2048^2 x 200)"}[args.arith],
                 "tblock": args.tblock,
                 "device": args.device,
                 "rehearsal_shared_gpu": bool(args.share_gpu),
@@ -364,12 +529,15 @@ def main() -> int:
             "native_selftest": (info["selftest"] if comm.size > 1 and on_gpu else None),
             "spinup_steps": spin,
         }
-        if secs_random is not None:
-            rec["ms_per_step_random"] = round(secs_random * 1e3 / args.steps, 4)
-            rec["value_random"] = round(pts * bpp * args.steps / secs_random / 1e9, 2)
-            rec["data_random"] = "synthetic random-init interior, uniform(0, 10), seed 1234 + rank, same BCs"
+        if headline_random:
+            rec["ms_per_step_uniform"] = round(secs_uniform * 1e3 / args.steps, 4)
+            rec["value_uniform"] = round(pts * bpp * args.steps / secs_uniform / 1e9, 2)
+            rec["data_uniform"] = "the reference's uniform IC 5.0, Dirichlet BCs 0/10/0/10"
+        for name, sf in secs_cmp.items():
+            rec[f"ms_per_step_{name}_{cmp_arith}"] = round(sf * 1e3 / args.steps, 4)
         if secs_dist1 is not None:
             rec["ms_per_step_dist_schedule"] = round(secs_dist1 * 1e3 / args.steps, 4)
+        rec.update(prims)
         print(json.dumps(rec), flush=True)
     sim.close_native()
     if dist.is_initialized():

@@ -118,7 +118,8 @@ def main():
         A = gens[name]()
         st = matrix_stats(A)
         auto = choose_format(A, st)
-        fmts = args.fmts or ["csr_scalar", "csr_vector", "csr_aligned", "csr_cb", "coo", "hyb", "ell", "dia"]
+        fmts = args.fmts or ["csr_scalar", "csr_vector", "csr_stream", "csr_aligned", "csr_cb", "coo", "hyb", "ell",
+                             "dia"]
         res = {}
         for f in fmts:
             if f == "ell" and (st.max_row > 64 or st.ell_fill < 0.3):
@@ -133,7 +134,7 @@ def main():
             sets = [(m, torch.rand(A.ncols, device="cuda"), torch.empty(A.nrows, device="cuda"))]
             for _ in range(reps - 1):
                 sets.append((clone(m), torch.rand(A.ncols, device="cuda"), torch.empty(A.nrows, device="cuda")))
-            kern = "scalar" if f == "csr_scalar" else "auto"
+            kern = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream"}.get(f, "auto")
 
             def cold():
                 for i in range(args.calls):

@@ -43,6 +43,7 @@
 // the transform is applied when pass 1 loads and undone when the last pass
 // stores, so no separate conversion kernels run. Optional 32-bit values.
 #include "cme213/common.h"
+#include "cme213/tuning.h"
 #include "cme213/lookback.h"
 #include "cme213/wave.h"
 
@@ -411,14 +412,23 @@ CME_EXPORT int cme_radix_onesweep(const uint32_t* kin, uint32_t* kout, uint32_t*
     // waves per SIMD = 2 blocks of 8 waves); the SGPR file (106 per wave: 6
     // waves per SIMD) does not, so the API's known over-report for SGPR-bound
     // kernels (common.h persistent_blocks_per_cu) does not apply here.
-    static const int bpc_k = occupancy_blocks_per_cu(radix_onesweep_kernel<false, true>, kOsThreads);
-    static const int bpc_kv = occupancy_blocks_per_cu(radix_onesweep_kernel<true, true>, kOsThreads);
+    // Per instantiation: the look-back needs every block of the grid resident,
+    // so the grid is sized for the kernel actually launched (the ballot-match
+    // fallback <V, false> may fit fewer blocks per CU than the lane-rank one;
+    // ADVICE r4)
+    static const int bpc[2][2] = {
+        {occupancy_blocks_per_cu(radix_onesweep_kernel<false, false>, kOsThreads),
+         occupancy_blocks_per_cu(radix_onesweep_kernel<false, true>, kOsThreads)},
+        {occupancy_blocks_per_cu(radix_onesweep_kernel<true, false>, kOsThreads),
+         occupancy_blocks_per_cu(radix_onesweep_kernel<true, true>, kOsThreads)}};
     // lane-order ranks where the device passed the check (not checked under
     // stream capture: a device not yet checked takes the ballot match)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-    const bool lanes = cme_radix_lane_order(capturing ? 0 : 1) != 0;
-    const long long cap = (long long)device_cu_count() * (vin ? bpc_kv : bpc_k);
+    const bool lanes = cme::tune_get(cme::kTuneRadixOsLanes) != 0 && cme_radix_lane_order(capturing ? 0 : 1) != 0;
+    const int bpc_used = bpc[vin ? 1 : 0][lanes ? 1 : 0];
+    if (bpc_used < 1) return (int)hipErrorInvalidConfiguration;
+    const long long cap = (long long)device_cu_count() * bpc_used;
     const int grid = (int)(tiles < cap ? tiles : cap);
     const uint32_t* src = kin;
     const uint32_t* vsrc = vin;

@@ -102,6 +102,86 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __r
     if (r < nrows && sub == 0) y[r] = beta == 0.f ? s : beta * y[r] + s;
 }
 
+// CSR-stream (short rows; the row-blocked scheme of CSR-adaptive): a
+// workgroup owns R consecutive rows. Its whole nonzero range [rp[r0],
+// rp[r0+R]) -- contiguous in col / val -- is streamed with coalesced loads,
+// every product val * x[col] lands in LDS, then T = 256 / R lanes per row sum
+// the row's products out of LDS and one coalesced store writes the R results.
+// CSR-vector gives each short row a whole group of lanes: on the 1M 5-point
+// Laplacian (5 nnz per row) 59 of its 64 lanes idle and every row issues its
+// own partial 4-B loads (389 GFLOP/s warm; refs/Bell SC 2009.pdf §3-4 names
+// this weakness of CSR-vector, refs/Baskaran IBM 2009.pdf pp.4-8 the
+// alignment cure). Here every lane of every load instruction carries a
+// useful nonzero. A block whose rows hold more than kStreamCap nonzeros
+// (skewed rows) falls back to one wave per row reading global memory, so any
+// CSR matrix is correct; the host picks R from the mean row length so that
+// R * mean sits well under the cap.
+constexpr int kStreamCap = 4096;  // products per block in LDS (16 KB)
+
+template <int R>
+__global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* __restrict__ rp,
+                                                         const int* __restrict__ col, const float* __restrict__ val,
+                                                         const float* __restrict__ x, float* __restrict__ y,
+                                                         float beta) {
+    static_assert(R == 64 || R == 128 || R == 256, "csr_stream: 64 / 128 / 256 rows per block");
+    constexpr int T = 256 / R;  // lanes per row in the reduction
+    __shared__ float prod[kStreamCap];
+    __shared__ int srp[R + 1];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * R;
+    const int nr = min(R, nrows - r0);
+    for (int i = tid; i <= nr; i += 256) srp[i] = rp[r0 + i];
+    __syncthreads();
+    const int base = srp[0];
+    const int nnz = srp[nr] - base;
+    if (nnz <= kStreamCap) {
+        // four coalesced (col, val) pairs per lane in flight, then their gathers
+        for (int j0 = 0; j0 < nnz; j0 += 4 * 256) {
+            int c[4];
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j0 + q * 256 + tid;
+                const bool ok = j < nnz;
+                c[q] = ok ? col[base + j] : 0;
+                v[q] = ok ? val[base + j] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j0 + q * 256 + tid;
+                if (j < nnz) prod[j] = v[q] * x[c[q]];
+            }
+        }
+        __syncthreads();
+        const int row = tid / T, sub = tid % T;
+        float s = 0.f;
+        if (row < nr) {
+            const int e = srp[row + 1] - base;
+            for (int j = srp[row] - base + sub; j < e; j += T) s += prod[j];
+        }
+#pragma unroll
+        for (int off = T / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (row < nr && sub == 0) {
+            float* yp = y + r0 + row;
+            *yp = beta == 0.f ? s : beta * *yp + s;
+        }
+        return;
+    }
+    // a block of long rows: one wave per row, 64 lanes strided over global
+    const int w = tid / 64, lane = tid % 64;
+    for (int row = w; row < nr; row += 4) {
+        const int b = srp[row], e = srp[row + 1];
+        float s = 0.f;
+        for (int j = b + lane; j < e; j += 64) s += val[j] * x[col[j]];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) {
+            float* yp = y + r0 + row;
+            *yp = beta == 0.f ? s : beta * *yp + s;
+        }
+    }
+}
+
 // All column / value loads of a group of 4 entries are issued before the
 // dependent x gathers (the row loop is a load-latency chain otherwise);
 // padding (col < 0) is masked without a branch. Summation order is k order.
@@ -303,6 +383,21 @@ CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const floa
     CME_LAUNCH_STATUS();
 }
 
+// CSR-stream: rows_per_block 64 / 128 / 256 (the host picks it from the mean
+// row length: csr_stream_kernel).
+CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, const float* val, const float* x,
+                                   float* y, int rows_per_block, float beta, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (nrows <= 0) return 0;
+    switch (rows_per_block) {
+#define V(R) case R: hipLaunchKernelGGL(csr_stream_kernel<R>, dim3(cdiv(nrows, R)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+        V(64) V(128) V(256)
+#undef V
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
+
 // Aligned CSR (every rp[i] % 4 == 0, col/val 16-B aligned): group 1..64;
 // nnz = col/val length (selects the stream loads).
 CME_EXPORT int cme_spmv_csr_aligned(int nrows, long long nnz, const int* rp, const int* col, const float* val,
@@ -378,3 +473,4 @@ CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);
 CME_REGISTER_KERNEL(spmv_dia, 256, dia_kernel);
 CME_REGISTER_KERNEL(spmv_dia4, 256, dia4_kernel);
 CME_REGISTER_KERNEL(spmv_coo, 256, coo_kernel);
+CME_REGISTER_KERNEL(spmv_csr_stream256, 256, csr_stream_kernel<256>);

@@ -34,6 +34,7 @@ enum TuneKey : int {
     kTuneSpmvDia1,         // CME_SPMV_DIA1
     kTunePipeTaper,        // CME_PIPE_TAPER: half-height last chunks per strip of a multi-round pass (0 off, -1 auto)
     kTuneRadixUpUnr,       // CME_RADIX_UP_UNR: radix upsweep 16-B loads in flight per lane (4, 8, 16)
+    kTuneRadixOsLanes,     // CME_RADIX_OS_LANES: onesweep ranks, 1 lane order where the probe passed, 0 ballot match
     kTuneCount
 };
 

@@ -313,3 +313,48 @@ def _ckpt_rank(rank, world, directory, tblock, use_async=False):
 @pytest.mark.parametrize("tblock,use_async", [(1, False), (2, False), (4, False), (2, True)])
 def test_dist_heat_checkpoint_restart_gloo(tmp_path, tblock, use_async):
     assert all(run_ranks(_ckpt_rank, 4, (str(tmp_path), tblock, use_async)))
+
+
+def _setup_agreement_rank(rank, world, fail_rank, fail_step):
+    import torch.distributed as dist
+
+    from cme213x.models.heat2d_dist import native_setup_agreement
+
+    calls = []
+
+    def agree(ok):
+        calls.append(ok)
+        t = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item() == 1.0)
+
+    def load_lib():
+        if rank == fail_rank and fail_step == "lib":
+            raise OSError("faked library-load failure")
+
+    opened = []
+
+    def open_transport():
+        if rank == fail_rank and fail_step == "transport":
+            raise RuntimeError("faked transport failure")
+        opened.append(True)
+        return "handle"
+
+    ok, handle = native_setup_agreement(agree, load_lib, open_transport, f"rank {rank}", "ipc")
+    # a collective after the setup: a rank left alone in one would hang here
+    t = torch.tensor([float(len(calls))])
+    dist.all_reduce(t)
+    return ok, len(calls), len(opened), float(t.item())
+
+
+@pytest.mark.parametrize("fail_rank,fail_step", [(1, "lib"), (0, "lib"), (1, "transport"), (-1, "")])
+def test_native_setup_every_rank_falls_back_together(fail_rank, fail_step):
+    """one rank failing to load the native library (or to open the
+    transport) makes EVERY rank fall back, after the same number of
+    agreement collectives -- no rank enters the self-test alone."""
+    parts = run_ranks(_setup_agreement_rank, 2, (fail_rank, fail_step))
+    oks = {p[0] for p in parts}
+    assert oks == {fail_rank < 0}
+    assert parts[0][1] == parts[1][1]  # same number of agree() calls on both ranks
+    if fail_step == "lib":
+        assert all(p[2] == 0 for p in parts)  # nobody opened a transport

@@ -138,6 +138,12 @@ def test_deep_passes_only_for_solo_fp32_gpu_pipe():
             DistHeat(p, None, f32, "cpu", tblock=6, kernel="pipe", **kw)
     with pytest.raises(ValueError, match="tblock"):
         DistHeat(p, None, torch.float64, "cpu", tblock=5, kernel="pipe")
+    # the reassociated pass stops at 4 steps: refused at construction (the
+    # check runs before any device allocation, so a CUDA device is fine here)
+    p8 = SimParams(nx=100, ny=100, order=8, iters=2, flavor="hw5")
+    for tb in (5, 6):
+        with pytest.raises(ValueError, match="fast"):
+            DistHeat(p8, None, f32, "cuda", tblock=tb, kernel="pipe", fma="fast")
 
 
 @pytest.mark.gpu

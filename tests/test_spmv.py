@@ -42,7 +42,8 @@ def test_csr_cpu_and_conversions():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
-@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_aligned", "ell", "dia", "coo", "hyb", "csr_cb"])
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_stream", "csr_auto", "csr_aligned", "ell", "dia", "coo",
+                                 "hyb", "csr_cb"])
 def test_spmv_gpu(gpu, mat, fmt):
     if mat == "5pt":
         a = laplacian("5pt", 100)
@@ -65,10 +66,11 @@ def test_spmv_gpu(gpu, mat, fmt):
         y1 = spmv(dev, x.to(gpu), y0.clone(), beta=0.5).cpu().numpy()
         np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
         return
-    dev = {"csr_scalar": a, "csr_vector": a, "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
+    dev = {"csr_scalar": a, "csr_vector": a, "csr_stream": a, "csr_auto": a,
+           "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
            "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
            "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
-    kernel = "scalar" if fmt == "csr_scalar" else "auto"
+    kernel = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream"}.get(fmt, "auto")
     y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
     np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
     # beta accumulate
@@ -138,3 +140,51 @@ def test_colblocked_needs_far_gathers():
     assert st.far_frac < 0.01 and st.ndiag > 64
     assert choose_format(a, st) == "csr_aligned"
     assert matrix_stats(random_csr(2000, 1 << 20, 12, seed=5)).far_frac > 0.8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows_case", ["long_rows", "empty_rows", "tail", "mixed"])
+def test_spmv_csr_stream_blocks(gpu, rows_case):
+    """CSR-stream's row blocks: a block whose nonzeros overflow the 4096-
+    product LDS buffer takes the wave-per-row fallback (rows of 3000 and 9000
+    entries among short ones), empty rows, a row count that is not a
+    multiple of the block, and every block size (64 / 128 / 256 rows by mean
+    row length) -- all against the fp64 oracle, with beta."""
+    from cme213x.ops.spmv import stream_rows
+
+    rng = np.random.default_rng(7)
+    n = 5003
+    if rows_case == "long_rows":
+        lens = rng.integers(1, 6, n)
+        lens[[17, 300, 301, 4000]] = [3000, 9000, 5000, 4097]
+    elif rows_case == "empty_rows":
+        lens = rng.integers(0, 3, n)
+    elif rows_case == "tail":
+        lens = np.full(n, 12)  # mean 12: 128-row blocks
+    else:
+        lens = rng.integers(10, 40, n)  # mean ~25: 64-row blocks
+    rows = np.repeat(np.arange(n), lens)
+    cols = rng.integers(0, 7000, rows.size)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    a = CSR(n, 7000, torch.from_numpy(rp), torch.from_numpy(cols.astype(np.int32)),
+            torch.from_numpy(rng.standard_normal(rows.size).astype(np.float32)))
+    x = torch.randn(a.ncols)
+    ref = _ref(a, x)
+    dev = a.to(gpu)
+    y = spmv(dev, x.to(gpu), kernel="stream").cpu().numpy()
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+    y0 = torch.randn(n, device=gpu)
+    y1 = spmv(dev, x.to(gpu), y0.clone(), kernel="stream", beta=0.5).cpu().numpy()
+    np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
+    assert stream_rows(a) in (64, 128, 256)
+
+
+def test_csr_auto_kernel_rule():
+    """CSR "auto" takes the stream kernel below a mean of 16 nonzeros per row
+    (rows per block from the mean), the vector kernel above."""
+    from cme213x.ops.spmv import STREAM_MAX_MEAN, stream_rows
+
+    assert STREAM_MAX_MEAN == 16
+    assert stream_rows(laplacian("5pt", 50)) == 256
+    assert stream_rows(random_csr(1000, 1000, 12, seed=1)) == 128
+    assert stream_rows(random_csr(1000, 1000, 30, seed=1)) == 64
