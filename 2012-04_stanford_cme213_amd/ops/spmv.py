@@ -312,12 +312,13 @@ def auto_group(a: CSR) -> int:
 
 
 def stream_rows(a: CSR) -> int:
-    """Rows per workgroup of the CSR-stream kernel: 256 / 128 / 64 for a mean
-    row length up to 8 / 16 / beyond, so a block's nonzeros (R x mean) stay
-    well inside its 4096-product LDS buffer (a heavier block still runs, on
-    the kernel's wave-per-row fallback)."""
+    """Rows per workgroup of the CSR-stream kernel: 512 / 256 / 128 / 64 for a
+    mean row length up to 6 / 12 / 24 / beyond, so a block's nonzeros (R x
+    mean) stay inside its 4096-product LDS buffer (a heavier block still
+    runs, on the kernel's wave-per-row fallback) while each block carries
+    enough entries to amortise its dependent rp -> col/val -> x round trips."""
     mean = a.nnz / max(1, a.nrows)
-    return 256 if mean <= 8 else (128 if mean <= 16 else 64)
+    return 512 if mean <= 6 else (256 if mean <= 12 else (128 if mean <= 24 else 64))
 
 
 # mean row length below which CSR "auto" takes the stream kernel

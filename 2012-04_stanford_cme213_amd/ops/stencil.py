@@ -37,6 +37,10 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f32", "ppiiiiiiiffp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f64", "ppiiiiiiiddp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_fast_f32", "ppiipipiiffiipupp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_fast_f32", "ppiiiiiiiiffipp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_f32", "ppiiiiiiiiiffip")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_trace_f32", "ppiiiiiiiiiffippp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_status", "pi")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_debug", "pi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -265,6 +269,51 @@ def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int]
         name = "cme_cpu_heat_run_f64" if f64 else "cme_cpu_heat_run_f32"
         _ext.call_cpu(name, a.data_ptr(), b.data_ptr(), pitch, xb, xe, yb, ye, order, xcfl, ycfl, iters)
     return a if iters % 2 == 0 else b
+
+
+def heat_flow(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
+              ycfl: float, npass: int, fma="fma", ns: int = 4, trace: bool = False):
+    """``npass`` four-step passes of the whole ``region`` as ONE persistent
+    dataflow launch (csrc/hip/heat_flow.hip: tasks pulled from a ticket, each
+    waiting for the 3 x 3 neighbourhood of the previous pass). fp32, order 8,
+    GPU; ``fma``: "exact" / False, "fma" / True, or "fast". Bit for bit the
+    result of ``npass`` one-pass launches (``heat_run`` with the knob
+    ``heat_flow`` = 0). Returns the buffer holding the result (``b`` for odd
+    ``npass``), or with ``trace=True`` ``(buffer, trace, tasks_per_pass)``:
+    trace[t] = (ticket time, start, end, HW_ID | XCC_ID << 32) of ticket t, in
+    100 MHz wall-clock ticks. Raises if a dependency wait gave up."""
+    _check(a, b)
+    if not a.is_cuda or a.dtype != torch.float32 or order != 8 or ns != 4:
+        raise ValueError("heat_flow: fp32, order 8, four steps per pass, on the GPU")
+    xb, xe, yb, ye = map(int, region)
+    rows, pitch = a.shape
+    code = arith_code(fma)
+    s = _ext.stream_ptr(a.device)
+    tr = None
+    if trace:
+        strips = -(-(xe - (xb & ~7)) // 480)
+        cap = strips * (-(-(ye - yb) // 16)) * int(npass)
+        tr = torch.zeros((cap, 4), dtype=torch.int64, device=a.device)
+        nt = ctypes.c_int(0)
+        _ext.call_hip("cme_heat_flow_trace_f32", a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, code,
+                      ns, xcfl, ycfl, int(npass), tr.data_ptr(), ctypes.addressof(nt), s)
+    else:
+        _ext.call_hip("cme_heat_flow_f32", a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, code, ns,
+                      xcfl, ycfl, int(npass), s)
+    torch.cuda.synchronize(a.device)
+    if flow_timed_out(reset=True):
+        raise RuntimeError("heat_flow: a dependency wait gave up (CME_FLOW_SPINS)")
+    out = b if npass % 2 else a
+    if trace:
+        return out, tr[: nt.value * int(npass)].cpu(), nt.value
+    return out
+
+
+def flow_timed_out(reset: bool = False) -> bool:
+    """Sticky give-up flag of the dataflow launches (read after a sync)."""
+    v = ctypes.c_uint(0)
+    _ext.call_hip("cme_heat_flow_status", ctypes.addressof(v), int(reset))
+    return bool(v.value)
 
 
 def heat_step_torch(prev: torch.Tensor, region, order: int, xcfl: float, ycfl: float) -> torch.Tensor:

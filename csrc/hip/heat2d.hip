@@ -982,6 +982,8 @@ CME_EXPORT int cme_heat_step_f64(const double* prev, double* curr, int pitch, in
                                  as_stream(stream));
 }
 
+extern "C" int cme_heat_flow_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
+                                 int arith, int ns, float xcfl, float ycfl, int npass, void* stream);
 extern "C" int cme_heat_tile_f32(const float* prev, float* curr, int pitch, int gy, int xb, int xe, int yb, int ye,
                                  int order, int nsteps, float xcfl, float ycfl, int fma, void* stream);
 extern "C" int cme_heat_tile_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb,
@@ -1027,6 +1029,20 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     if (variant >= 7 && variant <= 18) {
         if (sizeof(T) != 4 && (variant == 9 || variant == 10 || variant >= 15)) return (int)hipErrorInvalidValue;
         const int ns = variant >= 11 ? (variant - 11) / 2 + 3 : (variant <= 8 ? 3 : 4);
+        if constexpr (sizeof(T) == 4) {
+            // fp32 order-8 four-step passes: all whole passes as ONE persistent
+            // dataflow launch (heat_flow.hip; bitwise the same passes), the
+            // remainder below. CME_HEAT_FLOW=0 keeps a launch per pass.
+            if ((variant == 13 || variant == 14) && order == 8 && chunk <= 0 && iters >= 2 * ns &&
+                cme::tune_get(cme::kTuneHeatFlow) != 0) {
+                const int np = iters / ns;
+                const int rc = cme_heat_flow_f32(a, b, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, variant == 14 ? 1 : 0,
+                                                 ns, xcfl, ycfl, np, (void*)s);
+                if (rc) return rc;
+                cur = np & 1;
+                i = np * ns;
+            }
+        }
         for (; i + ns <= iters; i += ns) {
             int rc = dispatch_heat<T>(order, variant, bufs[cur], bufs[cur ^ 1], pitch, gy, g, xcfl, ycfl, chunk, s);
             if (rc) return rc;

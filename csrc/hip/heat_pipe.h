@@ -413,6 +413,50 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
     st.run_role(k);
 }
 
+// One strip-chunk task of region r of R (the whole workgroup): rows and
+// columns of the task, the interior / edge instantiation, the pass itself.
+// Shared by the one-pass launch (heat_pipe_kernel) and the persistent
+// multi-pass dataflow launch (heat_flow.hip).
+template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int WPR, int VW, bool LX, int NSLOT>
+__device__ __forceinline__ void pipe_task(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * WPR],
+                                          V4<T> (*edge)[3][RB][WPR][2], const S2Regions& R, int r, int task,
+                                          const T* prev, T* curr, int pitch, int gy, int xb1, int xe1, int yb1,
+                                          int ye1, T xcfl, T ycfl, int k, int sub, int lane) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    using G = PipeOut<NS, WPR, VW, B>;
+    constexpr int OUT = G::kOut;
+    constexpr int M = G::kMargin;
+    constexpr int LW = 64 * WPR;
+    const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
+    const int strips = R.strips[r];
+    // chunk word: rows per chunk in the low 16 bits; a tapered region
+    // (pipe_taper) keeps n1 = bits 16.. full chunks per strip and cuts the
+    // rest -- the tasks dispatched last -- to half height
+    const int chunk = R.chunk[r] & 0xffff, n1 = R.chunk[r] >> 16;
+    const int strip = task % strips;
+    const int ck = task / strips;
+    const bool half = n1 > 0 && ck >= n1;
+    const int y0 = half ? yb + n1 * chunk + (ck - n1) * (chunk >> 1) : yb + ck * chunk;
+    const int y1 = min(ye, y0 + (half ? chunk >> 1 : chunk));
+    const int xs = (xb & ~(VW - 1)) + strip * OUT;
+    const int gl = sub * 64 + lane;
+    const int xbase = xs - VW * M + VW * gl;
+    const int xl = min(max(xbase, 0), pitch - VW);
+    const bool out_lane = (gl >= M) && (gl <= LW - 1 - M) && (xbase < xe) && (xbase + VW > xb);
+    const bool full_vec = (xbase >= xb) && (xbase + VW <= xe);
+    constexpr int reach = 4 * (NS - 1);
+    const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
+                        (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
+    if (inside)
+        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
+                                                                 gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
+                                                                 xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+    else
+        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
+                                                                gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
+                                                                xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+}
+
 // one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for
 // streamN. VW = 8: strips start on 8-column boundaries, so every lane's
 // columns lie wholly inside or wholly outside the grid (the edge lanes' loads
@@ -426,11 +470,6 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
     constexpr int NSLOT = PipeN<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX>::NSLOT;
     __shared__ V4<T> ring[NS - 1][NSLOT][RB][VW / 4][64 * WPR];
     __shared__ V4<T> edge[WPR > 1 ? NS : 1][3][RB][WPR][2];
-    constexpr int B = HeatOrder<ORDER>::B;
-    using G = PipeOut<NS, WPR, VW, B>;
-    constexpr int OUT = G::kOut;
-    constexpr int M = G::kMargin;
-    constexpr int LW = 64 * WPR;
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
     const int k = wv / WPR, sub = wv % WPR;
@@ -462,34 +501,8 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the halo rows the exchange wrote, not stale L1 lines
     }
-    const int xb = R.xb[r], xe = R.xe[r], yb = R.yb[r], ye = R.ye[r];
-    const int strips = R.strips[r];
-    // chunk word: rows per chunk in the low 16 bits; a tapered region
-    // (pipe_taper) keeps n1 = bits 16.. full chunks per strip and cuts the
-    // rest -- the tasks dispatched last -- to half height
-    const int chunk = R.chunk[r] & 0xffff, n1 = R.chunk[r] >> 16;
-    const int strip = task % strips;
-    const int ck = task / strips;
-    const bool half = n1 > 0 && ck >= n1;
-    const int y0 = half ? yb + n1 * chunk + (ck - n1) * (chunk >> 1) : yb + ck * chunk;
-    const int y1 = min(ye, y0 + (half ? chunk >> 1 : chunk));
-    const int xs = (xb & ~(VW - 1)) + strip * OUT;
-    const int gl = sub * 64 + lane;
-    const int xbase = xs - VW * M + VW * gl;
-    const int xl = min(max(xbase, 0), pitch - VW);
-    const bool out_lane = (gl >= M) && (gl <= LW - 1 - M) && (xbase < xe) && (xbase + VW > xb);
-    const bool full_vec = (xbase >= xb) && (xbase + VW <= xe);
-    constexpr int reach = 4 * (NS - 1);
-    const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
-                        (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
-    if (inside)
-        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
-                                                                 gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
-                                                                 xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
-    else
-        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
-                                                                gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
-                                                                xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+    pipe_task<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, R, r, task, prev, curr, pitch, gy, xb1, xe1,
+                                                             yb1, ye1, xcfl, ycfl, k, sub, lane);
     if (gate.trace) {  // profiling: the whole workgroup's span (vector stores)
         __syncthreads();
         if (threadIdx.x == 0) {

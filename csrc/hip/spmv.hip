@@ -118,13 +118,19 @@ __global__ __launch_bounds__(256) void csr_vec4_kernel(int nrows, const int* __r
 // R * mean sits well under the cap.
 constexpr int kStreamCap = 4096;  // products per block in LDS (16 KB)
 
+// R rows per 256-lane workgroup: T = 256 / R lanes per row (R <= 256) or
+// R / 256 rows per lane (R = 512) in the reduction. The nonzero range is read
+// as 16-B (4-entry) pieces of col and val -- the aligned body of the range,
+// up to three pieces per lane in flight before their gathers -- plus a head
+// and a tail of at most 3 entries each read singly.
 template <int R>
 __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* __restrict__ rp,
                                                          const int* __restrict__ col, const float* __restrict__ val,
                                                          const float* __restrict__ x, float* __restrict__ y,
                                                          float beta) {
-    static_assert(R == 64 || R == 128 || R == 256, "csr_stream: 64 / 128 / 256 rows per block");
-    constexpr int T = 256 / R;  // lanes per row in the reduction
+    static_assert(R == 64 || R == 128 || R == 256 || R == 512, "csr_stream: 64 / 128 / 256 / 512 rows per block");
+    constexpr int T = R <= 256 ? 256 / R : 1;    // lanes per row
+    constexpr int RPT = R <= 256 ? 1 : R / 256;  // rows per lane
     __shared__ float prod[kStreamCap];
     __shared__ int srp[R + 1];
     const int tid = threadIdx.x;
@@ -133,37 +139,61 @@ __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* _
     for (int i = tid; i <= nr; i += 256) srp[i] = rp[r0 + i];
     __syncthreads();
     const int base = srp[0];
-    const int nnz = srp[nr] - base;
+    const int end = srp[nr];
+    const int nnz = end - base;
     if (nnz <= kStreamCap) {
-        // four coalesced (col, val) pairs per lane in flight, then their gathers
-        for (int j0 = 0; j0 < nnz; j0 += 4 * 256) {
-            int c[4];
-            float v[4];
+        const int a0 = min((base + 3) & ~3, end);  // first 16-B boundary of the range
+        const int a1 = max(end & ~3, a0);          // last
+        // head [base, a0) and tail [a1, end): at most 3 entries each
+        if (tid < a0 - base) prod[tid] = val[base + tid] * x[col[base + tid]];
+        if (tid >= 64 && tid - 64 < end - a1) {
+            const int j = a1 + tid - 64;
+            prod[j - base] = val[j] * x[col[j]];
+        }
+        const int npc = (a1 - a0) >> 2;  // 4-entry pieces of the aligned body
+        typedef int i32x4v __attribute__((ext_vector_type(4)));
+        typedef float f32x4v __attribute__((ext_vector_type(4)));
+        for (int p0 = 0; p0 < npc; p0 += 3 * 256) {
+            i32x4v c[3];
+            f32x4v v[3];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = j0 + q * 256 + tid;
-                const bool ok = j < nnz;
-                c[q] = ok ? col[base + j] : 0;
-                v[q] = ok ? val[base + j] : 0.f;
+            for (int q = 0; q < 3; ++q) {
+                const int pc = p0 + q * 256 + tid;
+                if (pc < npc) {
+                    c[q] = *reinterpret_cast<const i32x4v*>(col + a0 + 4 * pc);
+                    v[q] = *reinterpret_cast<const f32x4v*>(val + a0 + 4 * pc);
+                } else {
+                    c[q] = i32x4v{0, 0, 0, 0};
+                    v[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+                }
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = j0 + q * 256 + tid;
-                if (j < nnz) prod[j] = v[q] * x[c[q]];
+            for (int q = 0; q < 3; ++q) {
+                const int pc = p0 + q * 256 + tid;
+                if (pc < npc) {
+                    float* d = prod + (a0 - base) + 4 * pc;
+                    d[0] = v[q].x * x[c[q].x];
+                    d[1] = v[q].y * x[c[q].y];
+                    d[2] = v[q].z * x[c[q].z];
+                    d[3] = v[q].w * x[c[q].w];
+                }
             }
         }
         __syncthreads();
-        const int row = tid / T, sub = tid % T;
-        float s = 0.f;
-        if (row < nr) {
-            const int e = srp[row + 1] - base;
-            for (int j = srp[row] - base + sub; j < e; j += T) s += prod[j];
-        }
 #pragma unroll
-        for (int off = T / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (row < nr && sub == 0) {
-            float* yp = y + r0 + row;
-            *yp = beta == 0.f ? s : beta * *yp + s;
+        for (int k = 0; k < RPT; ++k) {
+            const int row = (RPT > 1 ? tid + k * 256 : tid / T), sub = tid % T;
+            float s = 0.f;
+            if (row < nr) {
+                const int e = srp[row + 1] - base;
+                for (int j = srp[row] - base + sub; j < e; j += T) s += prod[j];
+            }
+#pragma unroll
+            for (int off = T / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+            if (row < nr && sub == 0) {
+                float* yp = y + r0 + row;
+                *yp = beta == 0.f ? s : beta * *yp + s;
+            }
         }
         return;
     }
@@ -383,7 +413,7 @@ CME_EXPORT int cme_spmv_csr(int nrows, const int* rp, const int* col, const floa
     CME_LAUNCH_STATUS();
 }
 
-// CSR-stream: rows_per_block 64 / 128 / 256 (the host picks it from the mean
+// CSR-stream: rows_per_block 64 / 128 / 256 / 512 (the host picks it from the mean
 // row length: csr_stream_kernel).
 CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, const float* val, const float* x,
                                    float* y, int rows_per_block, float beta, void* stream) {
@@ -391,7 +421,7 @@ CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, con
     if (nrows <= 0) return 0;
     switch (rows_per_block) {
 #define V(R) case R: hipLaunchKernelGGL(csr_stream_kernel<R>, dim3(cdiv(nrows, R)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
-        V(64) V(128) V(256)
+        V(64) V(128) V(256) V(512)
 #undef V
         default: return (int)hipErrorInvalidValue;
     }

@@ -1,0 +1,132 @@
+"""Persistent dataflow schedule of the pipelined heat pass (csrc/hip/
+heat_flow.hip): all four-step passes of a run in ONE launch, tasks pulled
+from a ticket, each waiting for its 3 x 3 neighbourhood of the previous pass.
+
+Parity: the result must equal, bit for bit, the same passes launched one by
+one (knob heat_flow = 0) and the CPU oracle's single steps of the same
+arithmetic (the reference's 10-ULP check, hw/hw2/solution/
+2dHeat_solution.cu:690-710, is met with zero ULP). Uneven load: many tiny
+tasks (knob flow_per_cu) so dependency waits actually happen, odd region
+edges so edge tasks differ in cost."""
+import pytest
+import torch
+
+from cme213x.models.heat2d import HeatGrid
+from cme213x.ops.stencil import flow_timed_out, heat_flow, heat_run, heat_step
+from cme213x.utils.params import SimParams
+
+ARITH = {"exact": ("pipe4", "naive"), "fma": ("pipe4_fma", "fma"), "fast": ("pipe4_fast", "fast")}
+
+
+def _grid(n, m, device, seed):
+    p = SimParams(nx=n, ny=m, order=8, flavor="hw5")
+    g = HeatGrid(p, torch.float32, device)
+    gen = torch.Generator().manual_seed(seed)
+    r = torch.rand(g.buf[0].shape, generator=gen) * 10.0
+    g.buf[0].copy_(r.to(device))
+    g.buf[1].copy_(r.to(device))
+    return g
+
+
+def _per_pass(g, region, npass, arith):
+    """npass one-pass launches (the flow knob off)."""
+    from cme213x.utils import tuning
+
+    a, b = g.buf[0].clone(), g.buf[1].clone()
+    with tuning.override(heat_flow=0):
+        out = heat_run(a, b, region, 8, g.xcfl, g.ycfl, 4 * npass, ARITH[arith][0])
+    return out.clone()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith", ["fma", "fast", "exact"])
+@pytest.mark.parametrize("shape,npass", [((1500, 1100), 2), ((2000, 1703), 5), ((4096, 4096), 3)])
+def test_flow_equals_per_pass_launches(gpu, arith, shape, npass):
+    g = _grid(*shape, gpu, seed=npass)
+    region = g.interior
+    ref = _per_pass(g, region, npass, arith)
+    a, b = g.buf[0].clone(), g.buf[1].clone()
+    out = heat_flow(a, b, region, 8, g.xcfl, g.ycfl, npass, fma=arith)
+    assert out.data_ptr() == (b if npass % 2 else a).data_ptr()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arith", ["fma", "fast"])
+def test_flow_equals_cpu_oracle(gpu, arith):
+    """Against the CPU oracle's single steps (13 steps = three flow passes
+    + a one-step remainder through heat_run's default path)."""
+    n, m, iters = 700, 523, 13
+    c = _grid(n, m, "cpu", seed=3)
+    g = _grid(n, m, gpu, seed=3)
+    a, b = c.buf[0].clone(), c.buf[1].clone()
+    for i in range(iters):
+        src, dst = (a, b) if i % 2 == 0 else (b, a)
+        heat_step(src, dst, c.interior, 8, c.xcfl, c.ycfl, ARITH[arith][1])
+    ref = a if iters % 2 == 0 else b
+    out = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, ARITH[arith][0])
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_cu", [24, 64])
+def test_flow_many_small_tasks_uneven(gpu, per_cu):
+    """Many short tasks (16-40-row chunks: dependency waits on every pass
+    boundary, tasks of unequal cost at the ragged right and bottom edges) and
+    a sub-region that is not the whole interior."""
+    from cme213x.utils import tuning
+
+    g = _grid(3000, 2500, gpu, seed=9)
+    region = (13, 2900, 9, 2411)
+    ref = _per_pass(g, region, 6, "fma")
+    with tuning.override(flow_per_cu=per_cu):
+        for _ in range(2):
+            out = heat_flow(g.buf[0].clone(), g.buf[1].clone(), region, 8, g.xcfl, g.ycfl, 6, fma="fma")
+            assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+def test_flow_trace_and_schedule(gpu):
+    """The profiling launch records every ticket once; pass p + 1 of a task
+    starts only after its neighbourhood's pass p ended (wall clock)."""
+    g = _grid(2048, 2048, gpu, seed=4)
+    npass = 4
+    ref = _per_pass(g, g.interior, npass, "fma")
+    out, tr, tpp = heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, npass, fma="fma",
+                             trace=True)
+    assert torch.equal(out, ref)
+    assert tr.shape[0] == tpp * npass and bool((tr[:, 2] > 0).all())
+    assert bool((tr[:, 1] >= tr[:, 0]).all()) and bool((tr[:, 2] >= tr[:, 1]).all())
+    strips = 5  # ceil(2048 / 480)
+    nch = tpp // strips
+    for p in range(1, npass):
+        for t in range(tpp):
+            s, c = t % strips, t // strips
+            start = int(tr[p * tpp + t, 1])
+            for dc in (-1, 0, 1):
+                for ds in (-1, 0, 1):
+                    s2, c2 = s + ds, c + dc
+                    if 0 <= s2 < strips and 0 <= c2 < nch:
+                        assert start >= int(tr[(p - 1) * tpp + c2 * strips + s2, 2])
+
+
+@pytest.mark.gpu
+def test_flow_timeout_raises_and_drains(gpu):
+    """A dependency wait that gives up (knob flow_spins = 1) aborts every
+    workgroup (the grid drains, no hang) and raises; the next call runs."""
+    from cme213x.utils import tuning
+
+    g = _grid(4096, 4096, gpu, seed=5)
+    with tuning.override(flow_spins=1, flow_per_cu=32):
+        with pytest.raises(RuntimeError, match="gave up"):
+            for _ in range(5):  # a wait must have been needed at least once
+                heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 8, fma="fma")
+    assert not flow_timed_out()
+    ref = _per_pass(g, g.interior, 2, "fma")
+    assert torch.equal(heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 2), ref)
+
+
+def test_flow_refuses_other_shapes():
+    g = _grid(100, 100, "cpu", seed=1)
+    with pytest.raises(ValueError, match="fp32, order 8"):
+        heat_flow(g.buf[0], g.buf[1], g.interior, 8, g.xcfl, g.ycfl, 2)
