@@ -46,6 +46,7 @@ struct FlowArgs {
     unsigned* timeout;   // pinned host word: set when a wait gives up (sticky)
     unsigned spins;      // polls per wait before giving up
     int npass;
+    int mode;  // diagnostics (CME_FLOW_MODE): 1 system-scope release, 2 system-scope acquire, 4 every wave acquires
     unsigned long long* trace;  // profiling: per ticket {ticket time, start, end, HW_ID | XCC_ID << 32}
 };
 
@@ -76,6 +77,11 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         if (__hip_atomic_load(f.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) tk = total;
         s_ticket = tk;
         s_stop = 0;
+        // the ticket's LDS write must be complete before this wave reaches
+        // the barrier the other waves read it behind: the compiler emitted
+        // no lgkmcnt wait on this path, and other waves then ran with the
+        // previous ticket (two tasks computed wrong, ~1 run in 5 at 4096^2)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (f.trace) t_tk = wall_clock64();
     };
     if (threadIdx.x == 0) fetch();
@@ -92,6 +98,14 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
                 if (lane < 9) {
                     const int s2 = strip + lane % 3 - 1, c2 = ck + lane / 3 - 1;
                     if (s2 >= 0 && s2 < strips && c2 >= 0 && c2 < nch) w = f.done + c2 * strips + s2;
+                }
+                if ((f.mode & 64) && lane == 9) {  // diagnostics: the whole previous pass (per-pass counter)
+                    // spin until counter[pass - 1] == tpp
+                    const unsigned* cnt = f.done + tpp + 16 * 64 + (pass - 1);
+                    for (unsigned sp = 0; sp < f.spins; ++sp) {
+                        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)tpp) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
                 }
                 bool give_up = false;
                 for (unsigned spins = 0;; ++spins) {
@@ -132,14 +146,40 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
                     }
                     __builtin_amdgcn_s_sleep(2);
                 }
+                if (f.mode & 32) {  // diagnostics: linger ~4 us after the match
+                    const unsigned long long t0 = wall_clock64();
+                    while (wall_clock64() - t0 < 400) __builtin_amdgcn_s_sleep(4);
+                }
                 // ONE acquire after the match; its wait holds the barrier
                 // below until the L1 invalidate has completed
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (f.mode & 2)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                else
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (give_up && lane == 0) s_stop = 1;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
             __syncthreads();
             if (__builtin_amdgcn_readfirstlane(s_stop)) break;
+            if (f.mode & 4) {  // diagnostics: every wave acquires for itself
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        if (f.mode & 128) {  // diagnostics: the wait block's barrier + acquire for every task
+            if (wv == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+        }
+        if (f.mode & 256) __syncthreads();  // diagnostics: one more barrier
+        if (f.mode & 512) {  // diagnostics: zero the LDS ring
+            V4<T>* rr = &ring[0][0][0][0][0];
+            constexpr int nr = (int)(sizeof(ring) / sizeof(V4<T>));
+            for (int i = threadIdx.x; i < nr; i += NS * WPR * 64) rr[i] = V4<T>{};
+            __syncthreads();
         }
         unsigned long long t_start = 0;
         if (f.trace && threadIdx.x == 0) t_start = wall_clock64();
@@ -150,11 +190,24 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         // publish: every wave drains its stores (and its last loads of the
         // input this pass's successors overwrite), barrier, one lane releases
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
+        if (f.mode & 16) {  // diagnostics: every wave releases for itself
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (f.mode & 8) {  // diagnostics: linger ~4 us before the release
+                const unsigned long long t0 = wall_clock64();
+                while (wall_clock64() - t0 < 400) __builtin_amdgcn_s_sleep(4);
+            }
+            if (f.mode & 1)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            else
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(f.done + task, (unsigned)(pass + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f.mode & 64)
+                __hip_atomic_fetch_add(f.done + tpp + 16 * 64 + pass, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (f.trace) {  // profiling only (vector stores)
                 const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
                 const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
@@ -183,7 +236,7 @@ FlowWs& flow_ws() {
 
 int flow_prepare(size_t done_words, FlowWs** out) {
     FlowWs& w = flow_ws();
-    const size_t need = ((4 + done_words + 16 * 64 + 3) / 4) * 4;  // + 64 give-up records
+    const size_t need = ((4 + done_words + 16 * 64 + 1024 + 3) / 4) * 4;  // + 64 give-up records, pass counters
     if (w.words < need) {
         if (w.dev) CME_TRY(hipFree(w.dev));
         w.dev = nullptr;
@@ -246,6 +299,7 @@ int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npa
     const long sp = cme::tune_get(cme::kTuneFlowSpins);
     f.spins = sp > 0 ? (unsigned)sp : (1u << 22);
     f.npass = npass;
+    f.mode = (int)cme::tune_get(cme::kTuneFlowMode);
     f.trace = trace;
     const long grid = resident < tpp * npass ? resident : tpp * npass;
     if (ntasks_out) *ntasks_out = (int)tpp;

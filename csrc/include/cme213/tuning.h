@@ -38,6 +38,7 @@ enum TuneKey : int {
     kTuneHeatFlow,         // CME_HEAT_FLOW: 1 multi-pass heat runs as one persistent dataflow launch (heat_flow.hip), 0 a launch per pass
     kTuneFlowPerCU,        // CME_FLOW_PER_CU: task target per CU of the dataflow launch (0 = the pipelined pass's rule)
     kTuneFlowSpins,        // CME_FLOW_SPINS: polls of a dataflow dependency wait before it gives up
+    kTuneFlowMode,         // CME_FLOW_MODE: diagnostics of the dataflow hand-off (fence scopes)
     kTuneCount
 };
 
