@@ -20,11 +20,13 @@
 //    and strips of >= 16 columns that neighbourhood covers the read-after-
 //    write on the new input AND the write-after-read on the buffer this pass
 //    overwrites (the previous pass's input);
-//  * hand-off per the agent-scope release/acquire recipe (cdna_hip_
-//    programming.md §6 Guideline 16): every wave drains its stores, barrier,
-//    one lane releases (buffer_wbl2) and stores the completion word; the
-//    waiting wave polls relaxed, acquires once, barrier, then the task's
-//    loads.
+//  * hand-off per the write-through recipe (cdna_hip_programming.md §6
+//    Guideline 16, R1): the task's output rows are stored sc1 (write-
+//    through), every wave drains its stores, barrier, one lane stores the
+//    completion word (sc1); the waiting wave polls relaxed, acquires once
+//    (L1 invalidate), barrier, then the task's loads. (A release fence per
+//    task -- an L2 write-back -- made the launch slower than per-pass
+//    launches.)
 //
 // The tail of pass p now overlaps the head of pass p + 1; only the last pass
 // drains. Each task's arithmetic is heat_pipe.h's pipe_task, so the result is
@@ -46,11 +48,16 @@ struct FlowArgs {
     unsigned* timeout;   // pinned host word: set when a wait gives up (sticky)
     unsigned spins;      // polls per wait before giving up
     int npass;
-    int mode;  // diagnostics (CME_FLOW_MODE): 1 system-scope release, 2 system-scope acquire, 4 every wave acquires
+    // diagnostics (CME_FLOW_MODE): 1 agent-scope release fence, 2 system-scope
+    // acquire, 4 every wave acquires, 8 / 32 linger before the release /
+    // after the match, 16 every wave releases, 64 wait for the whole previous
+    // pass, 128 / 256 / 512 extra barrier + acquire / barrier / LDS ring
+    // reset at every task start, 2048 the first task never publishes
+    int mode;
     unsigned long long* trace;  // profiling: per ticket {ticket time, start, end, HW_ID | XCC_ID << 32}
 };
 
-template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int WPR, int VW, int OCC>
+template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int WPR, int VW, int OCC, int OST = 1>
 __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void heat_flow_kernel(
     T* a, T* b, int pitch, int gy, S2Regions R, int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl, FlowArgs f) {
     constexpr int NSLOT = PipeN<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, false>::NSLOT;
@@ -185,8 +192,12 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         if (f.trace && threadIdx.x == 0) t_start = wall_clock64();
         T* src = (pass & 1) ? b : a;
         T* dst = (pass & 1) ? a : b;
-        pipe_task<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, false, NSLOT>(ring, edge, R, 0, task, src, dst, pitch, gy,
-                                                                       xb1, xe1, yb1, ye1, xcfl, ycfl, k, sub, lane);
+        // output rows stored write-through (sc1), so the completion flag
+        // needs only the drain below, no L2 write-back fence (a release per
+        // task made the 16384^2 run 8 % slower than per-pass launches)
+        pipe_task<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, false, NSLOT, OST>(ring, edge, R, 0, task, src, dst, pitch, gy,
+                                                                          xb1, xe1, yb1, ye1, xcfl, ycfl, k, sub,
+                                                                          lane);
         // publish: every wave drains its stores (and its last loads of the
         // input this pass's successors overwrite), barrier, one lane releases
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -196,16 +207,19 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (f.mode & 8) {  // diagnostics: linger ~4 us before the release
+            if (f.mode & 8) {  // diagnostics: linger ~4 us before the publish
                 const unsigned long long t0 = wall_clock64();
                 while (wall_clock64() - t0 < 400) __builtin_amdgcn_s_sleep(4);
             }
-            if (f.mode & 1)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            else
+            if (OST == 0 || (f.mode & 1)) {  // plain / nt output stores: an agent-scope release fence
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(f.done + task, (unsigned)(pass + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const unsigned long long t_end = f.trace ? wall_clock64() : 0ull;  // before the flag
+            // (diagnostics, mode 2048: the first task never publishes, so a
+            // dependency wait must give up -- the timeout / drain test)
+            if (!((f.mode & 2048) && t == 0))
+                __hip_atomic_store(f.done + task, (unsigned)(pass + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (f.mode & 64)
                 __hip_atomic_fetch_add(f.done + tpp + 16 * 64 + pass, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (f.trace) {  // profiling only (vector stores)
@@ -214,7 +228,7 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
                 unsigned long long* tr = f.trace + 4ull * t;
                 tr[0] = t_tk;
                 tr[1] = t_start;
-                tr[2] = wall_clock64();
+                tr[2] = t_end;
                 tr[3] = ((unsigned long long)(xcc & 0xff) << 32) | hw;
             }
             fetch();
@@ -252,7 +266,7 @@ int flow_prepare(size_t done_words, FlowWs** out) {
     return 0;
 }
 
-template <typename T, int ORDER, int NS, int FMA, int RB, int PD, bool NT, int WPR, int VW, int OCC>
+template <typename T, int ORDER, int NS, int FMA, int RB, int PD, bool NT, int WPR, int VW, int OCC, int OST = 1>
 int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npass, hipStream_t s,
                 unsigned long long* trace, int* ntasks_out) {
     constexpr int B = HeatOrder<ORDER>::B;
@@ -260,10 +274,11 @@ int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npa
     static_assert(kOut >= 16, "flow: the strip neighbourhood must cover the pass's column reach");
     if (npass < 1) return 0;
     if ((pitch & 63) != 0) return (int)hipErrorInvalidValue;
+    if ((size_t)gy * pitch * sizeof(T) >= (1ull << 31)) return (int)hipErrorInvalidValue;  // 32-bit store offsets
     static const long resident = [] {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, heat_flow_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC>, NS * WPR * 64, 0) !=
+                &per_cu, heat_flow_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC, OST>, NS * WPR * 64, 0) !=
                 hipSuccess ||
             per_cu < 1)
             per_cu = 1;
@@ -303,7 +318,7 @@ int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npa
     f.trace = trace;
     const long grid = resident < tpp * npass ? resident : tpp * npass;
     if (ntasks_out) *ntasks_out = (int)tpp;
-    hipLaunchKernelGGL((heat_flow_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((heat_flow_kernel<T, ORDER, RB, NS, FMA, PD, NT, WPR, VW, OCC, OST>), dim3((unsigned)grid),
                        dim3(NS * WPR * 64), 0, s, a, b, pitch, gy, R, g.xb, g.xe, g.yb, g.ye, xcfl, ycfl, f);
     CME_LAUNCH_STATUS();
 }
@@ -318,7 +333,10 @@ int flow_f32(float* a, float* b, int pitch, int gy, Region g, int arith, int ns,
     if (ns != 4) return (int)hipErrorInvalidValue;
     switch (arith) {
         case 0: return launch_flow<float, 8, 4, 0, 2, 1, true, 1, 8, 0>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace, ntasks);
-        case 1: return launch_flow<float, 8, 4, 4, 2, 1, true, 1, 8, 0>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace, ntasks);
+        case 1:
+            if (cme::tune_get(cme::kTuneFlowMode) & 4096)  // diagnostics: nt stores + a release fence per task
+                return launch_flow<float, 8, 4, 4, 2, 1, true, 1, 8, 3, 0>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace, ntasks);
+            return launch_flow<float, 8, 4, 4, 2, 1, true, 1, 8, 3>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace, ntasks);
         case 2: return launch_flow<float, 8, 4, 5, 2, 1, true, 1, 8, 3>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace, ntasks);
         default: return (int)hipErrorInvalidValue;
     }
@@ -369,5 +387,5 @@ CME_EXPORT int cme_heat_flow_status(unsigned* timed_out, int reset) {
 }
 
 // kernels in the occupancy / resource report (cme_kernel_query)
-CME_REGISTER_KERNEL(heat_flow4_fma_f32_o8, 256, heat_flow_kernel<float, 8, 2, 4, 4, 1, true, 1, 8, 0>);
+CME_REGISTER_KERNEL(heat_flow4_fma_f32_o8, 256, heat_flow_kernel<float, 8, 2, 4, 4, 1, true, 1, 8, 3>);
 CME_REGISTER_KERNEL(heat_flow4_fast_f32_o8, 256, heat_flow_kernel<float, 8, 2, 4, 5, 1, true, 1, 8, 3>);

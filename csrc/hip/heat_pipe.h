@@ -69,7 +69,7 @@ __device__ __forceinline__ float uniform_f(float v) {
 // the VALU; the centre rows arrived B/RB phases earlier, so the ring keeps
 // 2 + B/RB slots. Role 0 (rows from HBM) keeps the DPP shifts.
 template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR = 1, int VW = 4,
-          bool LX = false>
+          bool LX = false, int OST = 0>
 struct PipeN {
     static constexpr int B = HeatOrder<ORDER>::B;
     static constexpr int NW = RB + 2 * B;
@@ -99,6 +99,12 @@ struct PipeN {
     Edge* edge;         // edge[k]: seam lanes of the step-k rows role k received (WPR > 1)
     const T* src;
     T* dst;
+    // OST = 1 (the dataflow launch's hand-off, heat_flow.hip): the output rows
+    // are stored write-through (sc1 buffer stores) from the uniform base
+    // `obase` at lane column `oxl`, so a completion flag needs no L2
+    // write-back fence behind them (cdna_hip_programming.md §6 Guideline 16, R1)
+    T* obase;
+    int oxl;
     int pitch, gy, xbase, lane, sub, glane, e3;
     int gl_l, gl_r;  // LX: the neighbour lanes (clamped into the strip; edge lanes are margin lanes)
     bool out_lane, full_vec;
@@ -229,6 +235,28 @@ struct PipeN {
         return o;
     }
 
+    // OST = 1: write-through stores of output row `row` (byte offsets fit 32
+    // bits: the launcher checks the buffer size)
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc() const {
+        return __builtin_amdgcn_make_buffer_rsrc(obase, (short)0, 0x7fffffff, 0x00020000);
+    }
+    __device__ __forceinline__ void store_out_wt(int row, const VT& o) const {
+        static_assert(sizeof(T) == 4, "write-through output stores: fp32");
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rs = out_rsrc();
+        const int off = (int)(((size_t)row * pitch + oxl) * sizeof(T));
+#pragma unroll
+        for (int h = 0; h < NH; ++h) {
+            const u32x4 v = {__builtin_bit_cast(unsigned, o[4 * h]), __builtin_bit_cast(unsigned, o[4 * h + 1]),
+                             __builtin_bit_cast(unsigned, o[4 * h + 2]), __builtin_bit_cast(unsigned, o[4 * h + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + 16 * h, 0, 16);
+        }
+    }
+    __device__ __forceinline__ void store_one_wt(int row, int j, T v) const {
+        const int off = (int)(((size_t)row * pitch + oxl + j) * sizeof(T));
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), out_rsrc(), off, 0, 16);
+    }
+
     __device__ __forceinline__ void store_out(T* d, const VT& o) const {
 #pragma unroll
         for (int h = 0; h < NH; ++h) {
@@ -305,7 +333,17 @@ struct PipeN {
                 else
                     o = upd<false>((S + i) % NW, row, ev[i]);
                 T* d = dst + (size_t)row * pitch;
-                if constexpr (!CHECK) {
+                if constexpr (OST == 1) {
+                    if (out_lane) {
+                        if (!CHECK || full_vec) {
+                            store_out_wt(row, o);
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < VW; ++j)
+                                if (xbase + j >= xb && xbase + j < xe) store_one_wt(row, j, o[j]);
+                        }
+                    }
+                } else if constexpr (!CHECK) {
                     if (out_lane) store_out(d, o);
                 } else if (out_lane) {
                     if (full_vec) {
@@ -370,13 +408,16 @@ struct PipeN {
 };
 
 template <typename T, int ORDER, int RB, int NS, int FMA, bool CHECK, int PD, bool NT, int WPR, int VW, bool LX,
-          int NSLOT>
+          int NSLOT, int OST = 0>
 __device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * WPR], V4<T> (*edge)[3][RB][WPR][2],
                                           int k, int sub, const T* src, T* dst, int pitch, int gy, int xbase,
                                           int lane, bool out_lane, bool full_vec, int y0, int y1, int xb, int xe,
-                                          int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl) {
-    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR, VW, LX> st;
+                                          int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl, T* obase = nullptr,
+                                          int oxl = 0) {
+    PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR, VW, LX, OST> st;
     static_assert(decltype(st)::NSLOT == NSLOT, "pipe: ring slots");
+    st.obase = obase;
+    st.oxl = oxl;
     st.ring = ring;
     st.edge = edge;
     st.sub = sub;
@@ -417,7 +458,8 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
 // columns of the task, the interior / edge instantiation, the pass itself.
 // Shared by the one-pass launch (heat_pipe_kernel) and the persistent
 // multi-pass dataflow launch (heat_flow.hip).
-template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int WPR, int VW, bool LX, int NSLOT>
+template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int WPR, int VW, bool LX, int NSLOT,
+          int OST = 0>
 __device__ __forceinline__ void pipe_task(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * WPR],
                                           V4<T> (*edge)[3][RB][WPR][2], const S2Regions& R, int r, int task,
                                           const T* prev, T* curr, int pitch, int gy, int xb1, int xe1, int yb1,
@@ -448,13 +490,13 @@ __device__ __forceinline__ void pipe_task(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
     const bool inside = (xs - reach >= xb1) && (xs + OUT + reach <= xe1) && (y0 - (NS - 1) * B >= yb1) &&
                         (y1 + (NS - 1) * B <= ye1) && (xs >= xb) && (xs + OUT <= xe);
     if (inside)
-        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
-                                                                 gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
-                                                                 xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+        pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT, OST>(
+            ring, edge, k, sub, prev + xl, curr + xl, pitch, gy, xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
+            xe1, yb1, ye1, xcfl, ycfl, curr, xl);
     else
-        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT>(ring, edge, k, sub, prev + xl, curr + xl, pitch,
-                                                                gy, xbase, lane, out_lane, full_vec, y0, y1, xb,
-                                                                xe, xb1, xe1, yb1, ye1, xcfl, ycfl);
+        pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT, OST>(
+            ring, edge, k, sub, prev + xl, curr + xl, pitch, gy, xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
+            xe1, yb1, ye1, xcfl, ycfl, curr, xl);
 }
 
 // one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for

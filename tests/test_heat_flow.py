@@ -117,10 +117,10 @@ def test_flow_timeout_raises_and_drains(gpu):
     from cme213x.utils import tuning
 
     g = _grid(4096, 4096, gpu, seed=5)
-    with tuning.override(flow_spins=1, flow_per_cu=32):
+    # diagnostics mode 2048: the first task never publishes its completion
+    with tuning.override(flow_spins=1 << 12, flow_mode=2048):
         with pytest.raises(RuntimeError, match="gave up"):
-            for _ in range(5):  # a wait must have been needed at least once
-                heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 8, fma="fma")
+            heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 8, fma="fma")
     assert not flow_timed_out()
     ref = _per_pass(g, g.interior, 2, "fma")
     assert torch.equal(heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 2), ref)
