@@ -102,6 +102,12 @@ def main():
             k += d
             m = max(m, k)
         conc.append(m)
+    # per XCD band: busy task time and the end of its last task
+    xcc = hw >> 32
+    rec["per_xcd_busy_ms"] = [round(float(dur[xcc == x].sum()) / 1e3, 1) for x in range(8)]
+    rec["per_xcd_last_end_us"] = [round(float(en[xcc == x].max()), 1) if (xcc == x).any() else None for x in range(8)]
+    rec["per_xcd_task_us_median"] = [round(float(np.median(dur[xcc == x])), 1) if (xcc == x).any() else None
+                                     for x in range(8)]
     rec["cus_seen"] = int(len(conc))
     rec["max_tasks_per_cu_hist"] = {str(v): int(c) for v, c in zip(*np.unique(conc, return_counts=True))}
     try:

@@ -9,6 +9,7 @@
 // Kernel template, chunk rule and launcher; the C entry points are in
 // heat_pipe.hip (production) and heat_pipe_tune.hip (tuning arms).
 #pragma once
+#include <limits.h>
 #include <stdlib.h>
 
 #include "cme213/common.h"
@@ -99,12 +100,14 @@ struct PipeN {
     Edge* edge;         // edge[k]: seam lanes of the step-k rows role k received (WPR > 1)
     const T* src;
     T* dst;
-    // OST = 1 (the dataflow launch's hand-off, heat_flow.hip): the output rows
-    // are stored write-through (sc1 buffer stores) from the uniform base
-    // `obase` at lane column `oxl`, so a completion flag needs no L2
-    // write-back fence behind them (cdna_hip_programming.md §6 Guideline 16, R1)
+    // OST = 1 / 2 (the dataflow launch's hand-off, heat_flow.hip): every
+    // output row / the rows outside [wt_lo, wt_hi) are stored write-through
+    // (sc1 buffer stores) from the uniform base `obase` at lane column `oxl`,
+    // so a completion flag needs no L2 write-back fence behind them for a
+    // reader on another XCD (cdna_hip_programming.md §6 Guideline 16, R1)
     T* obase;
     int oxl;
+    int wt_lo, wt_hi;  // OST = 2: rows outside [wt_lo, wt_hi) write-through, the rest as NT says
     int pitch, gy, xbase, lane, sub, glane, e3;
     int gl_l, gl_r;  // LX: the neighbour lanes (clamped into the strip; edge lanes are margin lanes)
     bool out_lane, full_vec;
@@ -333,14 +336,18 @@ struct PipeN {
                 else
                     o = upd<false>((S + i) % NW, row, ev[i]);
                 T* d = dst + (size_t)row * pitch;
-                if constexpr (OST == 1) {
-                    if (out_lane) {
-                        if (!CHECK || full_vec) {
-                            store_out_wt(row, o);
-                        } else {
+                bool wt = false;
+                if constexpr (OST != 0) wt = OST == 1 || row < wt_lo || row >= wt_hi;
+                if (wt) {
+                    if constexpr (OST != 0) {
+                        if (out_lane) {
+                            if (!CHECK || full_vec) {
+                                store_out_wt(row, o);
+                            } else {
 #pragma unroll
-                            for (int j = 0; j < VW; ++j)
-                                if (xbase + j >= xb && xbase + j < xe) store_one_wt(row, j, o[j]);
+                                for (int j = 0; j < VW; ++j)
+                                    if (xbase + j >= xb && xbase + j < xe) store_one_wt(row, j, o[j]);
+                            }
                         }
                     }
                 } else if constexpr (!CHECK) {
@@ -413,11 +420,13 @@ __device__ __forceinline__ void pipen_run(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
                                           int k, int sub, const T* src, T* dst, int pitch, int gy, int xbase,
                                           int lane, bool out_lane, bool full_vec, int y0, int y1, int xb, int xe,
                                           int xb1, int xe1, int yb1, int ye1, T xcfl, T ycfl, T* obase = nullptr,
-                                          int oxl = 0) {
+                                          int oxl = 0, int wt_lo = 0, int wt_hi = 0) {
     PipeN<T, ORDER, RB, NS, FMA, CHECK, PD, NT, WPR, VW, LX, OST> st;
     static_assert(decltype(st)::NSLOT == NSLOT, "pipe: ring slots");
     st.obase = obase;
     st.oxl = oxl;
+    st.wt_lo = wt_lo;
+    st.wt_hi = wt_hi;
     st.ring = ring;
     st.edge = edge;
     st.sub = sub;
@@ -463,7 +472,8 @@ template <typename T, int ORDER, int RB, int NS, int FMA, int PD, bool NT, int W
 __device__ __forceinline__ void pipe_task(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * WPR],
                                           V4<T> (*edge)[3][RB][WPR][2], const S2Regions& R, int r, int task,
                                           const T* prev, T* curr, int pitch, int gy, int xb1, int xe1, int yb1,
-                                          int ye1, T xcfl, T ycfl, int k, int sub, int lane) {
+                                          int ye1, T xcfl, T ycfl, int k, int sub, int lane, int wt_lo = 0,
+                                          int wt_hi = 0) {
     constexpr int B = HeatOrder<ORDER>::B;
     using G = PipeOut<NS, WPR, VW, B>;
     constexpr int OUT = G::kOut;
@@ -492,11 +502,11 @@ __device__ __forceinline__ void pipe_task(V4<T> (*ring)[NSLOT][RB][VW / 4][64 * 
     if (inside)
         pipen_run<T, ORDER, RB, NS, FMA, false, PD, NT, WPR, VW, LX, NSLOT, OST>(
             ring, edge, k, sub, prev + xl, curr + xl, pitch, gy, xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
-            xe1, yb1, ye1, xcfl, ycfl, curr, xl);
+            xe1, yb1, ye1, xcfl, ycfl, curr, xl, wt_lo, wt_hi);
     else
         pipen_run<T, ORDER, RB, NS, FMA, true, PD, NT, WPR, VW, LX, NSLOT, OST>(
             ring, edge, k, sub, prev + xl, curr + xl, pitch, gy, xbase, lane, out_lane, full_vec, y0, y1, xb, xe, xb1,
-            xe1, yb1, ye1, xcfl, ycfl, curr, xl);
+            xe1, yb1, ye1, xcfl, ycfl, curr, xl, wt_lo, wt_hi);
 }
 
 // one workgroup (NS roles x WPR waves) per strip-chunk task; regions as for

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTunePipeTaper,        // CME_PIPE_TAPER: half-height last chunks per strip of a multi-round pass (0 off, -1 auto)
     kTuneRadixUpUnr,       // CME_RADIX_UP_UNR: radix upsweep 16-B loads in flight per lane (4, 8, 16)
     kTuneRadixOsLanes,     // CME_RADIX_OS_LANES: onesweep ranks, 1 lane order where the probe passed, 0 ballot match
-    kTuneHeatFlow,         // CME_HEAT_FLOW: 1 multi-pass heat runs as one persistent dataflow launch (heat_flow.hip), 0 a launch per pass
+    kTuneHeatFlow,         // CME_HEAT_FLOW: 1 multi-pass heat runs as one persistent dataflow launch (heat_flow.hip), 0 (default) a launch per pass
     kTuneFlowPerCU,        // CME_FLOW_PER_CU: task target per CU of the dataflow launch (0 = the pipelined pass's rule)
     kTuneFlowSpins,        // CME_FLOW_SPINS: polls of a dataflow dependency wait before it gives up
     kTuneFlowMode,         // CME_FLOW_MODE: diagnostics of the dataflow hand-off (fence scopes)

@@ -55,7 +55,9 @@ def test_flow_equals_per_pass_launches(gpu, arith, shape, npass):
 @pytest.mark.parametrize("arith", ["fma", "fast"])
 def test_flow_equals_cpu_oracle(gpu, arith):
     """Against the CPU oracle's single steps (13 steps = three flow passes
-    + a one-step remainder through heat_run's default path)."""
+    + a one-step remainder through heat_run with the flow knob on)."""
+    from cme213x.utils import tuning
+
     n, m, iters = 700, 523, 13
     c = _grid(n, m, "cpu", seed=3)
     g = _grid(n, m, gpu, seed=3)
@@ -64,7 +66,8 @@ def test_flow_equals_cpu_oracle(gpu, arith):
         src, dst = (a, b) if i % 2 == 0 else (b, a)
         heat_step(src, dst, c.interior, 8, c.xcfl, c.ycfl, ARITH[arith][1])
     ref = a if iters % 2 == 0 else b
-    out = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, ARITH[arith][0])
+    with tuning.override(heat_flow=1):
+        out = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, ARITH[arith][0])
     assert torch.equal(out.cpu(), ref)
 
 
@@ -130,3 +133,20 @@ def test_flow_refuses_other_shapes():
     g = _grid(100, 100, "cpu", seed=1)
     with pytest.raises(ValueError, match="fp32, order 8"):
         heat_flow(g.buf[0], g.buf[1], g.interior, 8, g.xcfl, g.ycfl, 2)
+
+
+@pytest.mark.gpu
+def test_flow_banded_stress_distinct_buffers(gpu):
+    """The XCD-banded hand-off (band-edge rows write-through, no L2 write-
+    back) on buffers whose interiors differ, so a task reading a stale or
+    wrong buffer shows: 2 and 6 passes, several repetitions (the ticket race
+    fixed this round failed about one run in five here)."""
+    g = _grid(4096, 4096, gpu, seed=13)
+    xb, xe, yb, ye = g.interior
+    gen = torch.Generator().manual_seed(14)
+    g.buf[1, yb:ye, xb:xe] = (torch.rand((ye - yb, xe - xb), generator=gen) * 10.0).to(gpu)
+    for npass in (2, 6):
+        ref = _per_pass(g, g.interior, npass, "fma")
+        for _ in range(4):
+            out = heat_flow(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, npass, fma="fma")
+            assert torch.equal(out, ref)
