@@ -317,18 +317,26 @@ def stream_rows(a: CSR) -> int:
     mean) stay inside its 4096-product LDS buffer (a heavier block still
     runs, on the kernel's wave-per-row fallback) while each block carries
     enough entries to amortise its dependent rp -> col/val -> x round trips."""
+    from ..utils import tuning
+
+    forced = tuning.get("spmv_stream_rows") if a.rp.is_cuda else 0
+    if forced in (64, 128, 256, 512, 1024):
+        return forced
     mean = a.nnz / max(1, a.nrows)
     return 512 if mean <= 6 else (256 if mean <= 12 else (128 if mean <= 24 else 64))
 
 
-# mean row length below which CSR "auto" takes the stream kernel
-STREAM_MAX_MEAN = 16
+# mean row length below which CSR "auto" takes the stream kernel (measured,
+# cold / MALL defeated, profiles/spmv_stream_r5.md: 27-pt Laplacian, 26.5 per
+# row, stream 1005 vs vector 415 GFLOP/s; random 16 per row 299 vs 248; skewed
+# 20 per row 38 vs 15; 5-pt 678 vs 302)
+STREAM_MAX_MEAN = 32
 
 
 def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
     """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
     "scalar", "vector", "stream" (CSR-stream: row blocks staged through LDS),
-    or "auto" (stream for a mean row length below 16, where CSR-vector idles
+    or "auto" (stream for a mean row length below 32, where CSR-vector idles
     most of its lanes; vector with auto group above). To pick the FORMAT by
     the matrix structure, convert once with :func:`prepare`."""
     if y is None:

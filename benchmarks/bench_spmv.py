@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--calls", type=int, default=64)
     ap.add_argument("--out", default=None)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture (for rocprofv3 counter runs)")
+    ap.add_argument("--tune", nargs="*", default=[], help="tuning knobs name=value, e.g. spmv_stream_rows=1024")
     args = ap.parse_args()
     import torch
 
@@ -84,6 +85,11 @@ def main():
     from cme213x.ops.spmv import choose_format, laplacian, matrix_stats, prepare, random_csr, spmv
 
     out = open(args.out, "a") if args.out else None
+    from cme213x.utils import tuning
+
+    knobs = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
+    for k, v in knobs.items():
+        tuning.set(k, v)
 
     def emit(**kw):
         s = json.dumps(kw)
@@ -169,7 +175,7 @@ def main():
             del gc, gw
             mb1 = nbytes(m) + 4 * (A.ncols + A.nrows)
             res[f] = ms_cold
-            emit(bench="spmv", matrix=name, fmt=f, nnz=A.nnz, sets=len(sets), ms_cold=round(ms_cold, 5),
+            emit(bench="spmv", matrix=name, fmt=f, tune=knobs, nnz=A.nnz, sets=len(sets), ms_cold=round(ms_cold, 5),
                  ms_warm=round(ms_warm, 5), GFLOPs_cold=round(2 * A.nnz / ms_cold / 1e6, 1),
                  GFLOPs_warm=round(2 * A.nnz / ms_warm / 1e6, 1), min_bytes=mb1,
                  GBps_cold=round(mb1 / ms_cold / 1e6, 1), pct_copy_cold=round(100 * mb1 / ms_cold / 1e6 / copy_GBps, 1),

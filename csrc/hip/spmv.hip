@@ -128,7 +128,8 @@ __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* _
                                                          const int* __restrict__ col, const float* __restrict__ val,
                                                          const float* __restrict__ x, float* __restrict__ y,
                                                          float beta) {
-    static_assert(R == 64 || R == 128 || R == 256 || R == 512, "csr_stream: 64 / 128 / 256 / 512 rows per block");
+    static_assert(R == 64 || R == 128 || R == 256 || R == 512 || R == 1024,
+                  "csr_stream: 64 / 128 / 256 / 512 / 1024 rows per block");
     constexpr int T = R <= 256 ? 256 / R : 1;    // lanes per row
     constexpr int RPT = R <= 256 ? 1 : R / 256;  // rows per lane
     __shared__ float prod[kStreamCap];
@@ -136,11 +137,12 @@ __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* _
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * R;
     const int nr = min(R, nrows - r0);
-    for (int i = tid; i <= nr; i += 256) srp[i] = rp[r0 + i];
-    __syncthreads();
-    const int base = srp[0];
-    const int end = srp[nr];
+    // the range ends first (uniform: scalar loads), so the col / val loads
+    // issue beside the row-pointer loads instead of one round trip after them
+    const int base = __builtin_amdgcn_readfirstlane(rp[r0]);
+    const int end = __builtin_amdgcn_readfirstlane(rp[r0 + nr]);
     const int nnz = end - base;
+    for (int i = tid; i <= nr; i += 256) srp[i] = rp[r0 + i];
     if (nnz <= kStreamCap) {
         const int a0 = min((base + 3) & ~3, end);  // first 16-B boundary of the range
         const int a1 = max(end & ~3, a0);          // last
@@ -198,6 +200,7 @@ __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* _
         return;
     }
     // a block of long rows: one wave per row, 64 lanes strided over global
+    __syncthreads();  // the row pointers in LDS
     const int w = tid / 64, lane = tid % 64;
     for (int row = w; row < nr; row += 4) {
         const int b = srp[row], e = srp[row + 1];
@@ -421,7 +424,7 @@ CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, con
     if (nrows <= 0) return 0;
     switch (rows_per_block) {
 #define V(R) case R: hipLaunchKernelGGL(csr_stream_kernel<R>, dim3(cdiv(nrows, R)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
-        V(64) V(128) V(256) V(512)
+        V(64) V(128) V(256) V(512) V(1024)
 #undef V
         default: return (int)hipErrorInvalidValue;
     }

@@ -39,6 +39,7 @@ enum TuneKey : int {
     kTuneFlowPerCU,        // CME_FLOW_PER_CU: task target per CU of the dataflow launch (0 = the pipelined pass's rule)
     kTuneFlowSpins,        // CME_FLOW_SPINS: polls of a dataflow dependency wait before it gives up
     kTuneFlowMode,         // CME_FLOW_MODE: diagnostics of the dataflow hand-off (fence scopes)
+    kTuneSpmvStreamRows,   // CME_SPMV_STREAM_ROWS: CSR-stream rows per block (0 = by mean row length)
     kTuneCount
 };
 

@@ -180,11 +180,11 @@ def test_spmv_csr_stream_blocks(gpu, rows_case):
 
 
 def test_csr_auto_kernel_rule():
-    """CSR "auto" takes the stream kernel below a mean of 16 nonzeros per row
+    """CSR "auto" takes the stream kernel below a mean of 32 nonzeros per row
     (rows per block from the mean), the vector kernel above."""
     from cme213x.ops.spmv import STREAM_MAX_MEAN, stream_rows
 
-    assert STREAM_MAX_MEAN == 16
+    assert STREAM_MAX_MEAN == 32
     assert stream_rows(laplacian("5pt", 50)) == 512
     assert stream_rows(random_csr(1000, 1000, 8, seed=1)) == 256
     assert stream_rows(random_csr(1000, 1000, 14, seed=1)) == 128
