@@ -192,3 +192,60 @@ def test_dist_spmv_processes_one_gpu(gpu, world):
             np.testing.assert_allclose(y1, want, rtol=1e-5, atol=1e-5)
             np.testing.assert_array_equal(y1, y2)
         np.testing.assert_allclose(part, ref, rtol=1e-4, atol=1e-3)
+
+
+def _driver_plan_rank(rank, world, n, iters_a, iters_b):
+    """The driver's N-GPU bench plan on n^2: 1-D stripes, async, four steps
+    per pass on the pipelined kernel, FMA arithmetic, fused schedule, IPC."""
+    import torch
+
+    import cme213x  # noqa: F401
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+    from cme213x.parallel.ipc import NativeIpc
+    from cme213x.utils.params import SimParams
+
+    torch.cuda.set_device(0)
+    comm = TorchComm()
+    p = SimParams(nx=n, ny=n, order=8, iters=iters_a + iters_b, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0), grid_method=1,
+                  sync=False, flavor="hw5")
+    sim = DistHeat(p, comm, torch.float32, "cuda:0", tblock=4, fma=True, kernel="pipe")
+    _set_ic(sim, torch.float32)
+    ipc = NativeIpc()
+    sim.run_native(iters_a, ipc=ipc)
+    sim.run_native(iters_b, ipc=ipc)
+    sim.ipc_check()
+    sim.gate_check()
+    s = next(iter(sim.subs.values()))
+    H = s.grid.H
+    own = s.grid.buf[s.grid.cur, H:H + s.blk.ny, H:H + s.blk.nx].cpu().numpy()
+    ipc.close()
+    return s.blk.x0, s.blk.y0, own, DistHeat.schedule()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_ipc_eight_processes_driver_plan(gpu):
+    """the exact plan the driver's 8-GPU bench runs (8
+    processes, 1-D stripes, async, 4 steps per pass, pipelined kernel, fused
+    schedule, 16-row halos both sides of every stripe), here as 8 processes
+    on one GPU over the IPC transport on a 4096^2 grid (512-row stripes):
+    every rank's final stripe bitwise equal to the single-grid FMA oracle
+    after 9 + 8 steps (whole passes, a tail, a second call), and the fused
+    schedule ran after its queue probe passed."""
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.utils.params import SimParams
+
+    n, ia, ib = 4096, 9, 8
+    parts = run_ranks(_driver_plan_rank, 8, (n, ia, ib), timeout=280)
+    p = SimParams(nx=n, ny=n, order=8, iters=ia + ib, ic=5.0, bc=(0.0, 10.0, 0.0, 10.0), grid_method=1, sync=False,
+                  flavor="hw5")
+    ref = DistHeat(p, None, torch.float32, "cpu", variant="naive", fma=True)
+    _set_ic(ref, torch.float32)
+    ref.run(p.iters)
+    st = ref.gather_global()
+    B = p.border
+    for r, (x0, y0, own, sch) in enumerate(parts):
+        want = st[B + y0:B + y0 + own.shape[0], B + x0:B + x0 + own.shape[1]]
+        assert np.array_equal(own, want), f"rank {r} ({sch}): max |diff| {np.abs(own - want).max()}"
+        assert sch["schedule"] == "fused" and sch["probe"] == "passed", sch
