@@ -41,6 +41,9 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_f32", "ppiiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_trace_f32", "ppiiiiiiiiiffippp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_status", "pi")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_debug", "pi")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_f64", "ppiiiiiiiiiddippp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_f32", "ppiiiiiiiiiffippp")
+_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_status", "pi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -313,6 +316,55 @@ def flow_timed_out(reset: bool = False) -> bool:
     """Sticky give-up flag of the dataflow launches (read after a sync)."""
     v = ctypes.c_uint(0)
     _ext.call_hip("cme_heat_flow_status", ctypes.addressof(v), int(reset))
+    return bool(v.value)
+
+
+HIP_COOP_TOO_LARGE = 720  # hipErrorCooperativeLaunchTooLarge
+
+
+def heat_tile_res(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
+                  ycfl: float, npass: int, ns: int = 2, fma: bool = False, trace: bool = False):
+    """``npass`` passes of ``ns`` (2, or 4 at order 8) steps of the whole
+    ``region`` with every 64 x 64 tile resident in LDS for the whole run, in
+    ONE cooperative launch (csrc/hip/heat_tile_res.hip: only the NS*B-deep
+    halo ring moves, behind the tile's inner cone). GPU, fp32 / fp64, orders
+    2 / 4 / 8; bit for bit the result of single steps of the same arithmetic.
+    Returns the buffer holding the result (``b`` for odd ``npass``), or with
+    ``trace=True`` ``(buffer, trace, ntiles)``: trace[pass * ntiles + tile,
+    :5] = wall-clock stamps (100 MHz) at the pass start, after the inner
+    steps, with the halo in, after the outer steps (ring stores issued), and
+    when the pass's ring was published (during the next pass). Raises ``RuntimeError`` if a
+    neighbour wait gave up, ``ValueError`` if the tiles cannot all be
+    resident (too large a grid: run tile passes)."""
+    _check(a, b)
+    if not a.is_cuda or order not in (2, 4, 8) or ns not in ((2, 4) if order == 8 else (2,)):
+        raise ValueError("heat_tile_res: GPU, orders 2/4/8, 2 steps per exchange (or 4 at order 8)")
+    xb, xe, yb, ye = map(int, region)
+    rows, pitch = a.shape
+    ntiles = (-(-(xe - xb) // 64)) * (-(-(ye - yb) // 64))
+    tr = torch.zeros((ntiles * int(npass), 8), dtype=torch.int64, device=a.device) if trace else None
+    nt = ctypes.c_int(0)
+    name = "cme_heat_tile_res_f64" if a.dtype == torch.float64 else "cme_heat_tile_res_f32"
+    rc = _ext._fn("hip", name)(a.data_ptr(), b.data_ptr(), pitch, rows, xb, xe, yb, ye, order, ns, int(bool(fma)),
+                               xcfl, ycfl, int(npass), tr.data_ptr() if trace else None, ctypes.addressof(nt),
+                               _ext.stream_ptr(a.device))
+    if rc == HIP_COOP_TOO_LARGE:
+        raise ValueError(f"heat_tile_res: {ntiles} tiles cannot all be resident on this device")
+    _ext.check(rc, name)
+    torch.cuda.synchronize(a.device)
+    if tile_res_timed_out(reset=True):
+        raise RuntimeError("heat_tile_res: a neighbour wait gave up (CME_FLOW_SPINS)")
+    out = b if npass % 2 else a
+    if trace:
+        return out, tr[:, :5].cpu(), nt.value
+    return out
+
+
+def tile_res_timed_out(reset: bool = False) -> bool:
+    """Sticky give-up flag of the resident-tile launches (read after a sync;
+    ``heat_run``'s tile variants use them)."""
+    v = ctypes.c_uint(0)
+    _ext.call_hip("cme_heat_tile_res_status", ctypes.addressof(v), int(reset))
     return bool(v.value)
 
 

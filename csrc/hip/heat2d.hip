@@ -988,6 +988,12 @@ extern "C" int cme_heat_tile_f32(const float* prev, float* curr, int pitch, int 
                                  int order, int nsteps, float xcfl, float ycfl, int fma, void* stream);
 extern "C" int cme_heat_tile_f64(const double* prev, double* curr, int pitch, int gy, int xb, int xe, int yb,
                                  int ye, int order, int nsteps, double xcfl, double ycfl, int fma, void* stream);
+extern "C" int cme_heat_tile_res_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
+                                     int ns, int fma, float xcfl, float ycfl, int npass, unsigned long long* trace,
+                                     int* ntiles, void* stream);
+extern "C" int cme_heat_tile_res_f64(double* a, double* b, int pitch, int gy, int xb, int xe, int yb, int ye,
+                                     int order, int ns, int fma, double xcfl, double ycfl, int npass,
+                                     unsigned long long* trace, int* ntiles, void* stream);
 
 namespace {
 int tile_pass_t(const float* p, float* c, int pitch, int gy, Region g, int order, int ns, int fma, float xc,
@@ -998,6 +1004,16 @@ int tile_pass_t(const double* p, double* c, int pitch, int gy, Region g, int ord
                 double yc, hipStream_t s) {
     return cme_heat_tile_f64(p, c, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, ns, xc, yc, fma, (void*)s);
 }
+int tile_res_t(float* a, float* b, int pitch, int gy, Region g, int order, int ns, int fma, float xc, float yc,
+               int npass, hipStream_t s) {
+    return cme_heat_tile_res_f32(a, b, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, ns, fma, xc, yc, npass, nullptr,
+                                 nullptr, (void*)s);
+}
+int tile_res_t(double* a, double* b, int pitch, int gy, Region g, int order, int ns, int fma, double xc, double yc,
+               int npass, hipStream_t s) {
+    return cme_heat_tile_res_f64(a, b, pitch, gy, g.xb, g.xe, g.yb, g.ye, order, ns, fma, xc, yc, npass, nullptr,
+                                 nullptr, (void*)s);
+}
 }  // namespace
 
 // Multi-step driver: `iters` sweeps of the full region in one call (buffers
@@ -1006,7 +1022,11 @@ int tile_pass_t(const double* p, double* c, int pitch, int gy, Region g, int ord
 // variants 4/5 advance TWO steps per launch (+ one single step, variant 2/6,
 // for odd iters). Variants 19..26: tileN exact / FMA, N = 1..4 steps per
 // pass of the LDS-resident tile kernel (heat_tile.hip, small grids), the
-// remainder as one shorter tile pass.
+// remainder as one shorter tile pass. With N >= 2 and the knob CME_TILE_RES
+// on (default off: measured slower, profiles/heat_tile_res_r5.md), the whole
+// passes run as ONE launch with the tiles resident in LDS (heat_tile_res.hip,
+// CME_TILE_RES_NS steps per halo exchange; bitwise the same steps) where
+// every tile fits on the device at once, tile passes otherwise.
 // *final_idx = 0 if the result is in a, 1 if in b.
 template <typename T>
 int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int variant, T xcfl, T ycfl, int iters,
@@ -1016,6 +1036,17 @@ int heat_run_impl(T* a, T* b, int pitch, int gy, Region g, int order, int varian
     int i = 0;
     if (variant >= 19 && variant <= 26) {
         const int ns = (variant - 19) / 2 + 1, fma = (variant - 19) & 1;
+        const int rns = (int)cme::tune_get(cme::kTuneTileResNs);
+        if (ns >= 2 && cme::tune_get(cme::kTuneTileRes) != 0 && (rns == 2 || (rns == 4 && order == 8)) && iters >= rns) {
+            const int np = iters / rns;
+            const int rc = tile_res_t(a, b, pitch, gy, g, order, rns, fma, xcfl, ycfl, np, s);
+            if (rc == 0) {
+                cur = np & 1;
+                i = np * rns;
+            } else if (rc != (int)hipErrorCooperativeLaunchTooLarge) {
+                return rc;
+            }
+        }
         while (i < iters) {
             const int k = iters - i < ns ? iters - i : ns;
             int rc = tile_pass_t(bufs[cur], bufs[cur ^ 1], pitch, gy, g, order, k, fma, xcfl, ycfl, s);

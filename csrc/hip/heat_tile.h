@@ -25,14 +25,97 @@ struct TileGeom {
     static_assert(TX % 2 == 0, "column pairs");
 };
 
+// One thread's share of a timestep: the column pair c0, c0 + 1 (w0 / w1:
+// which of the two lies inside the step's region) over rows [rb, re) of the
+// LDS tile, from src into dst.
+template <typename T, int ORDER, bool FMA, int PW>
+__device__ __forceinline__ void tile_band(const T* __restrict__ src, T* __restrict__ dst, int c0, int rb, int re,
+                                          bool w0, bool w1, T xcfl, T ycfl) {
+    constexpr int B = HeatOrder<ORDER>::B;
+    constexpr int RING = 2 * B + 2;
+    constexpr int NXP = (B + 1) / 2;  // x-neighbour pairs on each side
+    const Pair<T>* s2 = reinterpret_cast<const Pair<T>*>(src);
+    Pair<T>* d2 = reinterpret_cast<Pair<T>*>(dst);
+    const int cp = c0 >> 1;  // pair column
+    // Register ring of RING = 2B + 2 row pairs (one more than the
+    // stencil's 2B + 1): row x sits in slot (x - (rb - B)) % RING, and
+    // row r + 1 + B is loaded into the free slot while row r computes;
+    // the x-neighbour pairs are double-buffered by row parity. The row
+    // loop is unrolled by RING (even), so every slot index is a
+    // compile-time constant: no register moves. LDS addresses are one
+    // row pointer plus immediate offsets.
+    constexpr int P = PW / 2;  // pairs per LDS row
+    Pair<T> win[RING];
+    Pair<T> xl[2][NXP], xr[2][NXP];
+    {
+        const Pair<T>* rp = s2 + (rb - B) * P + cp;
+#pragma unroll
+        for (int k = 0; k <= 2 * B; ++k) win[k] = rp[k * P];
+        rp += B * P;  // row rb
+#pragma unroll
+        for (int q = 0; q < NXP; ++q) {
+            xl[0][q] = rp[-1 - q];  // columns c0-2-2q, c0-1-2q
+            xr[0][q] = rp[1 + q];   // columns c0+2+2q, c0+3+2q
+        }
+    }
+    for (int r0 = rb; r0 < re; r0 += RING) {
+        // one base address per RING rows: every load below is base +
+        // a compile-time (non-negative) offset
+        const Pair<T>* base = s2 + (r0 + 1) * P + cp - NXP;
+        Pair<T>* dbase = d2 + r0 * P + cp;
+        // row guards against one count (u < rem): row u's prefetch guard
+        // is row u + 1's compute guard, one compare per row, no row index
+        const int rem = re - r0;
+#pragma unroll
+        for (int u = 0; u < RING; ++u) {
+            if (u < rem) {
+                if (u + 1 < rem) {  // prefetch row r + 1: its x pairs, and row r + 1 + B into the free slot
+                    const Pair<T>* rp = base + u * P;  // pair column c0 / 2 - NXP of row r + 1
+                    win[(u + 1 + 2 * B) % RING] = rp[B * P + NXP];
+#pragma unroll
+                    for (int q = 0; q < NXP; ++q) {
+                        xl[(u + 1) & 1][q] = rp[NXP - 1 - q];
+                        xr[(u + 1) & 1][q] = rp[NXP + 1 + q];
+                    }
+                }
+                const Pair<T>(&XL)[NXP] = xl[u & 1];
+                const Pair<T>(&XR)[NXP] = xr[u & 1];
+                const Pair<T> c = win[(u + B) % RING];
+                T out[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    T xm[B], xp[B], ym[B], yp[B];
+#pragma unroll
+                    for (int k = 0; k < B; ++k) {
+                        // x of column c0 + j - (k + 1) and c0 + j + (k + 1)
+                        const int dm = j - (k + 1), dp = j + (k + 1);  // offsets from c0
+                        xm[k] = dm >= 0 ? c.v[dm] : XL[(-dm - 1) / 2].v[1 - ((-dm - 1) & 1)];
+                        xp[k] = dp <= 1 ? c.v[dp] : XR[(dp - 2) / 2].v[(dp - 2) & 1];
+                        ym[k] = win[(u + B - (k + 1) + RING) % RING].v[j];
+                        yp[k] = win[(u + B + (k + 1)) % RING].v[j];
+                    }
+                    out[j] = heat_update_sel<ORDER, FMA>(c.v[j], xm, xp, ym, yp, xcfl, ycfl);
+                }
+                if (w0 && w1) {
+                    Pair<T> o;
+                    o.v[0] = out[0];
+                    o.v[1] = out[1];
+                    dbase[u * P] = o;
+                } else {
+                    const int r = r0 + u;
+                    if (w0) dst[r * PW + c0] = out[0];
+                    if (w1) dst[r * PW + c0 + 1] = out[1];
+                }
+            }
+        }
+    }
+}
+
 // One timestep of the tile: rows [r_lo, r_hi) x columns [c_lo, c_hi) (LDS
 // coordinates) from src into dst.
 template <typename T, int ORDER, bool FMA, int PW, int NT>
 __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restrict__ dst, int c_lo, int c_hi, int r_lo,
                                           int r_hi, T xcfl, T ycfl) {
-    constexpr int B = HeatOrder<ORDER>::B;
-    constexpr int RING = 2 * B + 2;
-    constexpr int NXP = (B + 1) / 2;  // x-neighbour pairs on each side
     if (c_hi <= c_lo || r_hi <= r_lo) return;
     const int ca = c_lo & ~1;
     const int npairs = (c_hi - ca + 1) >> 1;
@@ -46,80 +129,39 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
         const int rb = r_lo + band * R;
         const int re = min(r_hi, rb + R);
         if (rb >= re) continue;
-        const bool w0 = c0 >= c_lo, w1 = c0 + 1 < c_hi;
-        const Pair<T>* s2 = reinterpret_cast<const Pair<T>*>(src);
-        Pair<T>* d2 = reinterpret_cast<Pair<T>*>(dst);
-        const int cp = c0 >> 1;  // pair column
-        // Register ring of RING = 2B + 2 row pairs (one more than the
-        // stencil's 2B + 1): row x sits in slot (x - (rb - B)) % RING, and
-        // row r + 1 + B is loaded into the free slot while row r computes;
-        // the x-neighbour pairs are double-buffered by row parity. The row
-        // loop is unrolled by RING (even), so every slot index is a
-        // compile-time constant: no register moves. LDS addresses are one
-        // row pointer plus immediate offsets.
-        constexpr int P = PW / 2;  // pairs per LDS row
-        Pair<T> win[RING];
-        Pair<T> xl[2][NXP], xr[2][NXP];
-        {
-            const Pair<T>* rp = s2 + (rb - B) * P + cp;
+        tile_band<T, ORDER, FMA, PW>(src, dst, c0, rb, re, c0 >= c_lo, c0 + 1 < c_hi, xcfl, ycfl);
+    }
+}
+
+// Tile + halo from global memory into both LDS buffers: LDS (0, 0) is grid
+// cell (gx0, gy0); cells outside the grid buffer read as 0 (a point inside
+// the region never reads them: the ghost layer stops every cone). Loads in
+// batches of kLB per thread, all issued before their LDS stores, so the
+// memory latency is paid once per batch, not once per element.
+template <typename T, int LW, int LH, int PW, int NT>
+__device__ __forceinline__ void tile_load(const T* __restrict__ prev, T* L0, T* L1, int gx0, int gy0, int pitch,
+                                          int gy) {
+    constexpr int kN = LH * LW;
+    // every load of the tile in flight at once where it fits (9 per thread
+    // for the production 64 x 64, NS = 4, 1024-thread shape: one memory
+    // latency instead of two; the trace had the 8-per-batch load at 2.2 us)
+    constexpr int kLB = (kN + NT - 1) / NT < 16 ? (kN + NT - 1) / NT : 16;
+    for (int i0 = 0; i0 < kN; i0 += NT * kLB) {
+        T v[kLB];
 #pragma unroll
-            for (int k = 0; k <= 2 * B; ++k) win[k] = rp[k * P];
-            rp += B * P;  // row rb
-#pragma unroll
-            for (int q = 0; q < NXP; ++q) {
-                xl[0][q] = rp[-1 - q];  // columns c0-2-2q, c0-1-2q
-                xr[0][q] = rp[1 + q];   // columns c0+2+2q, c0+3+2q
-            }
+        for (int k = 0; k < kLB; ++k) {
+            const int i = i0 + k * NT + (int)threadIdx.x;
+            const int r = i / LW, c = i - r * LW;
+            const int x = gx0 + c, y = gy0 + r;
+            v[k] = (i < kN && x >= 0 && x < pitch && y >= 0 && y < gy) ? prev[(size_t)y * pitch + x] : T(0);
         }
-        for (int r0 = rb; r0 < re; r0 += RING) {
-            // one base address per RING rows: every load below is base +
-            // a compile-time (non-negative) offset
-            const Pair<T>* base = s2 + (r0 + 1) * P + cp - NXP;
-            Pair<T>* dbase = d2 + r0 * P + cp;
-            // row guards against one count (u < rem): row u's prefetch guard
-            // is row u + 1's compute guard, one compare per row, no row index
-            const int rem = re - r0;
 #pragma unroll
-            for (int u = 0; u < RING; ++u) {
-                if (u < rem) {
-                    if (u + 1 < rem) {  // prefetch row r + 1: its x pairs, and row r + 1 + B into the free slot
-                        const Pair<T>* rp = base + u * P;  // pair column c0 / 2 - NXP of row r + 1
-                        win[(u + 1 + 2 * B) % RING] = rp[B * P + NXP];
-#pragma unroll
-                        for (int q = 0; q < NXP; ++q) {
-                            xl[(u + 1) & 1][q] = rp[NXP - 1 - q];
-                            xr[(u + 1) & 1][q] = rp[NXP + 1 + q];
-                        }
-                    }
-                    const Pair<T>(&XL)[NXP] = xl[u & 1];
-                    const Pair<T>(&XR)[NXP] = xr[u & 1];
-                    const Pair<T> c = win[(u + B) % RING];
-                    T out[2];
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        T xm[B], xp[B], ym[B], yp[B];
-#pragma unroll
-                        for (int k = 0; k < B; ++k) {
-                            // x of column c0 + j - (k + 1) and c0 + j + (k + 1)
-                            const int dm = j - (k + 1), dp = j + (k + 1);  // offsets from c0
-                            xm[k] = dm >= 0 ? c.v[dm] : XL[(-dm - 1) / 2].v[1 - ((-dm - 1) & 1)];
-                            xp[k] = dp <= 1 ? c.v[dp] : XR[(dp - 2) / 2].v[(dp - 2) & 1];
-                            ym[k] = win[(u + B - (k + 1) + RING) % RING].v[j];
-                            yp[k] = win[(u + B + (k + 1)) % RING].v[j];
-                        }
-                        out[j] = heat_update_sel<ORDER, FMA>(c.v[j], xm, xp, ym, yp, xcfl, ycfl);
-                    }
-                    if (w0 && w1) {
-                        Pair<T> o;
-                        o.v[0] = out[0];
-                        o.v[1] = out[1];
-                        dbase[u * P] = o;
-                    } else {
-                        const int r = r0 + u;
-                        if (w0) dst[r * PW + c0] = out[0];
-                        if (w1) dst[r * PW + c0 + 1] = out[1];
-                    }
-                }
+        for (int k = 0; k < kLB; ++k) {
+            const int i = i0 + k * NT + (int)threadIdx.x;
+            if (i < kN) {
+                const int r = i / LW, c = i - r * LW;
+                L0[r * PW + c] = v[k];
+                L1[r * PW + c] = v[k];
             }
         }
     }
@@ -151,34 +193,7 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     const int txi = (int)blockIdx.x - tyi * tiles_x;
     const int ox = g.xb + txi * TX, oy = g.yb + tyi * TY;  // output origin (grid)
     const int gx0 = ox - H, gy0 = oy - H;                  // LDS (0, 0) in grid coordinates
-    // tile + halo into both buffers (cells outside the grid buffer are never
-    // read by a point inside g: the ghost layer stops every cone). Loads in
-    // batches of kLB per thread, all issued before their LDS stores, so the
-    // memory latency is paid once per batch, not once per element.
-    constexpr int kN = LH * LW;
-    // every load of the tile in flight at once where it fits (9 per thread
-    // for the production 64 x 64, NS = 4, 1024-thread shape: one memory
-    // latency instead of two; the trace had the 8-per-batch load at 2.2 us)
-    constexpr int kLB = (kN + NT - 1) / NT < 16 ? (kN + NT - 1) / NT : 16;
-    for (int i0 = 0; i0 < kN; i0 += NT * kLB) {
-        T v[kLB];
-#pragma unroll
-        for (int k = 0; k < kLB; ++k) {
-            const int i = i0 + k * NT + (int)threadIdx.x;
-            const int r = i / LW, c = i - r * LW;
-            const int x = gx0 + c, y = gy0 + r;
-            v[k] = (i < kN && x >= 0 && x < pitch && y >= 0 && y < gy) ? prev[(size_t)y * pitch + x] : T(0);
-        }
-#pragma unroll
-        for (int k = 0; k < kLB; ++k) {
-            const int i = i0 + k * NT + (int)threadIdx.x;
-            if (i < kN) {
-                const int r = i / LW, c = i - r * LW;
-                L0[r * PW + c] = v[k];
-                L1[r * PW + c] = v[k];
-            }
-        }
-    }
+    tile_load<T, LW, LH, PW, NT>(prev, L0, L1, gx0, gy0, pitch, gy);
     __syncthreads();
     if (trace && threadIdx.x == 0) tr[1] = wall_clock64();
     // region g in LDS coordinates

@@ -40,6 +40,9 @@ enum TuneKey : int {
     kTuneFlowSpins,        // CME_FLOW_SPINS: polls of a dataflow dependency wait before it gives up
     kTuneFlowMode,         // CME_FLOW_MODE: diagnostics of the dataflow hand-off (fence scopes)
     kTuneSpmvStreamRows,   // CME_SPMV_STREAM_ROWS: CSR-stream rows per block (0 = by mean row length)
+    kTuneTileRes,          // CME_TILE_RES: 1 tileN heat runs keep the tiles resident in LDS across passes (heat_tile_res.hip; default 0: measured slower)
+    kTuneTileResNs,        // CME_TILE_RES_NS: steps per halo exchange of the resident tiles (2 or 4)
+    kTuneTileResMinR,      // CME_TILE_RES_MINR: rows per band at least in the resident tiles' steps
     kTuneCount
 };
 
