@@ -22,6 +22,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_spmv_coo", "iqpppppfip")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "iqpppppifp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_stream", "ipppppifp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_short", "ipppppifp")
 
 
 # ---------------------------------------------------------------- formats
@@ -333,9 +334,18 @@ def stream_rows(a: CSR) -> int:
 STREAM_MAX_MEAN = 32
 
 
+def short_rows_per_lane(a: CSR) -> int:
+    """Rows per lane of the CSR-short kernel (tuning knob spmv_short_rpt)."""
+    from ..utils import tuning
+
+    r = tuning.get("spmv_short_rpt") if a.rp.is_cuda else 1
+    return r if r in (1, 2, 4) else 1
+
+
 def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
     """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
     "scalar", "vector", "stream" (CSR-stream: row blocks staged through LDS),
+    "short" (a lane per row, the first 8 entries of a row as one batch of loads),
     or "auto" (stream for a mean row length below 32, where CSR-vector idles
     most of its lanes; vector with auto group above). To pick the FORMAT by
     the matrix structure, convert once with :func:`prepare`."""
@@ -357,6 +367,9 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
         g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
         _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.nnz, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), g, float(beta), s)
+    elif isinstance(a, CSR) and kernel == "short":
+        _ext.call_hip("cme_spmv_csr_short", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), short_rows_per_lane(a), float(beta), s)
     elif isinstance(a, CSR) and (kernel == "stream" or
                                  (kernel == "auto" and a.nnz < STREAM_MAX_MEAN * max(1, a.nrows))):
         _ext.call_hip("cme_spmv_csr_stream", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
@@ -463,6 +476,7 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
         m = to_csr_colblocked(a, int(parts[0]) << 10, aligned=not (len(parts) > 1 and parts[1] == "u"))
         return fmt, (m.to(device) if device is not None else m)
     conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_stream": lambda m: m,
+            "csr_short": lambda m: m,
             "csr_aligned": to_csr_aligned,
             "csr_cb": to_csr_colblocked,
             "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}

@@ -215,6 +215,58 @@ __global__ __launch_bounds__(256) void csr_stream_kernel(int nrows, const int* _
     }
 }
 
+// CSR-short (mean row length <= 8, the 5-point Laplacian of config #4): one
+// lane per row and RPT rows per lane (rows r0 + t + 256 k, so every load
+// instruction of a wave walks consecutive rows). A row's first kShortNB
+// entries are ONE batch of guarded col / val loads -- the row length comes
+// with the row pointers -- so a 5-entry row costs three dependent round trips
+// (rp, then col / val, then x) where csr_scalar's 4-entry loop plus remainder
+// costs five; RPT rows per lane put every round trip of the lane's rows in
+// flight together (half the waves, each with twice the loads outstanding).
+// Entries past kShortNB (long rows) run a loop. Summation in entry order.
+constexpr int kShortNB = 8;
+
+template <int RPT>
+__global__ __launch_bounds__(256) void csr_short_kernel(int nrows, const int* __restrict__ rp,
+                                                        const int* __restrict__ col, const float* __restrict__ val,
+                                                        const float* __restrict__ x, float* __restrict__ y,
+                                                        float beta) {
+    const int r0 = blockIdx.x * (256 * RPT) + threadIdx.x;
+    int b[RPT], e[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int r = r0 + 256 * k;
+        b[k] = r < nrows ? rp[r] : 0;
+        e[k] = r < nrows ? rp[r + 1] : 0;
+    }
+    int c[RPT][kShortNB];
+    float v[RPT][kShortNB];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+        for (int q = 0; q < kShortNB; ++q) {
+            const bool in = b[k] + q < e[k];
+            c[k][q] = in ? col[b[k] + q] : -1;
+            v[k][q] = in ? val[b[k] + q] : 0.f;
+        }
+    float xv[RPT][kShortNB];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+        for (int q = 0; q < kShortNB; ++q) xv[k][q] = c[k][q] >= 0 ? x[c[k][q]] : 0.f;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int r = r0 + 256 * k;
+        if (r >= nrows) continue;
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < kShortNB; ++q)
+            if (c[k][q] >= 0) s += v[k][q] * xv[k][q];
+        for (int j = b[k] + kShortNB; j < e[k]; ++j) s += val[j] * x[col[j]];
+        y[r] = beta == 0.f ? s : beta * y[r] + s;
+    }
+}
+
 // All column / value loads of a group of 4 entries are issued before the
 // dependent x gathers (the row loop is a load-latency chain otherwise);
 // padding (col < 0) is masked without a branch. Summation order is k order.
@@ -431,6 +483,20 @@ CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, con
     CME_LAUNCH_STATUS();
 }
 
+// CSR-short: rows_per_lane 1 / 2 / 4 (csr_short_kernel).
+CME_EXPORT int cme_spmv_csr_short(int nrows, const int* rp, const int* col, const float* val, const float* x,
+                                  float* y, int rows_per_lane, float beta, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (nrows <= 0) return 0;
+    switch (rows_per_lane) {
+#define V(R) case R: hipLaunchKernelGGL(csr_short_kernel<R>, dim3(cdiv(nrows, 256 * R)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta); break;
+        V(1) V(2) V(4)
+#undef V
+        default: return (int)hipErrorInvalidValue;
+    }
+    CME_LAUNCH_STATUS();
+}
+
 // Aligned CSR (every rp[i] % 4 == 0, col/val 16-B aligned): group 1..64;
 // nnz = col/val length (selects the stream loads).
 CME_EXPORT int cme_spmv_csr_aligned(int nrows, long long nnz, const int* rp, const int* col, const float* val,
@@ -500,6 +566,7 @@ CME_EXPORT int cme_spmv_coo(int nrows, long long nnz, const int* row, const int*
 
 // kernels in the occupancy / resource report (cme_kernel_query)
 CME_REGISTER_KERNEL(spmv_csr_scalar, 256, csr_scalar_kernel);
+CME_REGISTER_KERNEL(spmv_csr_short2, 256, csr_short_kernel<2>);
 CME_REGISTER_KERNEL(spmv_csr_vector8, 256, csr_vector_kernel<8>);
 CME_REGISTER_KERNEL(spmv_csr_aligned4, 256, csr_vec4_kernel<4, true>);
 CME_REGISTER_KERNEL(spmv_ell, 256, ell_kernel);

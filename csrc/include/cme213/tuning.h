@@ -43,6 +43,7 @@ enum TuneKey : int {
     kTuneTileRes,          // CME_TILE_RES: 1 tileN heat runs keep the tiles resident in LDS across passes (heat_tile_res.hip; default 0: measured slower)
     kTuneTileResNs,        // CME_TILE_RES_NS: steps per halo exchange of the resident tiles (2 or 4)
     kTuneTileResMinR,      // CME_TILE_RES_MINR: rows per band at least in the resident tiles' steps
+    kTuneSpmvShortRpt,     // CME_SPMV_SHORT_RPT: CSR-short rows per lane (1, 2, 4)
     kTuneCount
 };
 

@@ -42,7 +42,8 @@ def test_csr_cpu_and_conversions():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
-@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_stream", "csr_auto", "csr_aligned", "ell", "dia", "coo",
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_stream", "csr_short", "csr_auto", "csr_aligned", "ell",
+                                 "dia", "coo",
                                  "hyb", "csr_cb"])
 def test_spmv_gpu(gpu, mat, fmt):
     if mat == "5pt":
@@ -66,11 +67,12 @@ def test_spmv_gpu(gpu, mat, fmt):
         y1 = spmv(dev, x.to(gpu), y0.clone(), beta=0.5).cpu().numpy()
         np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
         return
-    dev = {"csr_scalar": a, "csr_vector": a, "csr_stream": a, "csr_auto": a,
+    dev = {"csr_scalar": a, "csr_vector": a, "csr_stream": a, "csr_short": a, "csr_auto": a,
            "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
            "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
            "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
-    kernel = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream"}.get(fmt, "auto")
+    kernel = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream", "csr_short": "short"}.get(fmt,
+                                                                                                           "auto")
     y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
     np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
     # beta accumulate
@@ -144,13 +146,19 @@ def test_colblocked_needs_far_gathers():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows_case", ["long_rows", "empty_rows", "tail", "mixed"])
-def test_spmv_csr_stream_blocks(gpu, rows_case):
+@pytest.mark.parametrize("kernel,rpt", [("stream", 0), ("short", 1), ("short", 2), ("short", 4)])
+def test_spmv_csr_stream_blocks(gpu, rows_case, kernel, rpt):
     """CSR-stream's row blocks: a block whose nonzeros overflow the 4096-
     product LDS buffer takes the wave-per-row fallback (rows of 3000 and 9000
     entries among short ones), empty rows, a row count that is not a
     multiple of the block, and every block size (64 / 128 / 256 rows by mean
-    row length) -- all against the fp64 oracle, with beta."""
+    row length) -- all against the fp64 oracle, with beta. The same matrices
+    through CSR-short (rows longer than its 8-entry batch, 1 / 2 / 4 rows per
+    lane, a ragged last block)."""
+    import contextlib
+
     from cme213x.ops.spmv import stream_rows
+    from cme213x.utils import tuning
 
     rng = np.random.default_rng(7)
     n = 5003
@@ -171,10 +179,11 @@ def test_spmv_csr_stream_blocks(gpu, rows_case):
     x = torch.randn(a.ncols)
     ref = _ref(a, x)
     dev = a.to(gpu)
-    y = spmv(dev, x.to(gpu), kernel="stream").cpu().numpy()
-    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
-    y0 = torch.randn(n, device=gpu)
-    y1 = spmv(dev, x.to(gpu), y0.clone(), kernel="stream", beta=0.5).cpu().numpy()
+    with tuning.override(spmv_short_rpt=rpt) if rpt else contextlib.nullcontext():
+        y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
+        np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
+        y0 = torch.randn(n, device=gpu)
+        y1 = spmv(dev, x.to(gpu), y0.clone(), kernel=kernel, beta=0.5).cpu().numpy()
     np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
     assert stream_rows(a) in (64, 128, 256, 512)
 

@@ -63,7 +63,10 @@ def test_gpu_tree_reduction_beats_serial(gpu):
     assert r["gpu_tree"] < r["serial"] and r["gpu_vector"] < r["serial"]
 
 
-_SPILL_OK = {"heat_pipe4w_fast_f32_o8": 64}
+# the dataflow launch of the reassociated pass (heat_flow.hip, off by
+# default) carries the ticket / wait / write-through state on top of the same
+# 3-waves-per-SIMD cap: measured at parity with per-pass launches anyway
+_SPILL_OK = {"heat_pipe4w_fast_f32_o8": 64, "heat_flow4_fast_f32_o8": 320}
 
 
 @pytest.mark.gpu
