@@ -123,8 +123,14 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
     nb = nb < 1 ? 1 : nb;
     const int rows = r_hi - r_lo;
     const int R = (rows + nb - 1) / nb;
+    // band = task / npairs through a float reciprocal (3 VALU instead of a
+    // ~20-instruction integer division per thread and step): task < NT and
+    // npairs <= 64, so (task + 0.5) / npairs sits >= 1/128 from an integer and
+    // the float error (< 2^-12 here) cannot cross it
+    static_assert(NT <= 4096, "tile_step: the reciprocal band index needs task < 4096");
+    const float inv_np = 1.0f / (float)npairs;
     for (int task = threadIdx.x; task < npairs * nb; task += NT) {
-        const int band = task / npairs;
+        const int band = (int)(((float)task + 0.5f) * inv_np);
         const int c0 = ca + 2 * (task - band * npairs);
         const int rb = r_lo + band * R;
         const int re = min(r_hi, rb + R);
@@ -141,6 +147,37 @@ __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restri
 template <typename T, int LW, int LH, int PW, int NT>
 __device__ __forceinline__ void tile_load(const T* __restrict__ prev, T* L0, T* L1, int gx0, int gy0, int pitch,
                                           int gy) {
+    if constexpr (LW % 2 == 0) {
+        // 16-B (fp64) / 8-B (fp32) column pairs where the tile's first column,
+        // the pitch and the buffer are pair-aligned (every production shape):
+        // half the loads, and the index math of one element per pair
+        if (((gx0 | pitch) & 1) == 0 && ((uintptr_t)prev % (2 * sizeof(T))) == 0) {
+            constexpr int LP = LW / 2, kP = LH * LP;
+            constexpr int kLB = (kP + NT - 1) / NT < 16 ? (kP + NT - 1) / NT : 16;
+            const Pair<T>* p2 = reinterpret_cast<const Pair<T>*>(prev);
+            for (int i0 = 0; i0 < kP; i0 += NT * kLB) {
+                Pair<T> v[kLB];
+#pragma unroll
+                for (int k = 0; k < kLB; ++k) {
+                    const int i = i0 + k * NT + (int)threadIdx.x;
+                    const int r = i / LP, cp = i - r * LP;
+                    const int x = gx0 + 2 * cp, y = gy0 + r;  // x even: x < pitch covers x + 1
+                    const bool in = i < kP && x >= 0 && x < pitch && y >= 0 && y < gy;
+                    v[k] = in ? p2[((size_t)y * pitch + x) >> 1] : Pair<T>{{T(0), T(0)}};
+                }
+#pragma unroll
+                for (int k = 0; k < kLB; ++k) {
+                    const int i = i0 + k * NT + (int)threadIdx.x;
+                    if (i < kP) {
+                        const int r = i / LP, cp = i - r * LP;
+                        reinterpret_cast<Pair<T>*>(L0 + r * PW)[cp] = v[k];
+                        reinterpret_cast<Pair<T>*>(L1 + r * PW)[cp] = v[k];
+                    }
+                }
+            }
+            return;
+        }
+    }
     constexpr int kN = LH * LW;
     // every load of the tile in flight at once where it fits (9 per thread
     // for the production 64 x 64, NS = 4, 1024-thread shape: one memory
@@ -211,7 +248,26 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     const int c_lo = max(H, gxl), c_hi = min(H + TX, gxh);
     const int r_lo = max(H, gyl), r_hi = min(H + TY, gyh);
     const int w = c_hi - c_lo;
-    if (w > 0 && r_hi > r_lo) {
+    // a whole tile (every tile but the ragged right / bottom ones) goes out as
+    // column pairs with a compile-time row length
+    bool whole = w == TX && r_hi - r_lo == TY && ((gx0 | pitch) & 1) == 0 &&
+                 ((uintptr_t)curr % (2 * sizeof(T))) == 0;
+    if constexpr (H % 2 != 0) whole = false;
+    if (whole) {
+        if constexpr (H % 2 == 0) {
+            typedef T T2 __attribute__((ext_vector_type(2)));
+            constexpr int TP = TX / 2;
+            for (int i = threadIdx.x; i < TP * TY; i += NT) {
+                const int r = H + i / TP, cp = H / 2 + i % TP;
+                const T2 v = reinterpret_cast<const T2*>(fin + r * PW)[cp];
+                T2* d = reinterpret_cast<T2*>(curr + (size_t)(gy0 + r) * pitch + gx0) + cp;
+                if constexpr (NTS)
+                    __builtin_nontemporal_store(v, d);
+                else
+                    *d = v;
+            }
+        }
+    } else if (w > 0 && r_hi > r_lo) {
         for (int i = threadIdx.x; i < w * (r_hi - r_lo); i += NT) {
             const int r = r_lo + i / w, c = c_lo + i % w;
             T* d = curr + (size_t)(gy0 + r) * pitch + gx0 + c;

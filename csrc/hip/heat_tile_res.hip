@@ -87,7 +87,7 @@ __device__ __forceinline__ void rects_step(const T* __restrict__ src, T* __restr
     for (int i = 0; i < NR; ++i) {
         const int n = np[i] * ((nr[i] + R - 1) / R);
         if (!mine && t < n) {
-            const int band = t / np[i];
+            const int band = (int)(((float)t + 0.5f) / (float)np[i]);  // t < NT, np <= 64: exact (tile_step)
             c0 = (q[i].c_lo & ~1) + 2 * (t - band * np[i]);
             rb = q[i].r_lo + band * R;
             re = min(q[i].r_hi, rb + R);
