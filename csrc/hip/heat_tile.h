@@ -111,24 +111,42 @@ __device__ __forceinline__ void tile_band(const T* __restrict__ src, T* __restri
     }
 }
 
+// How a step's region is dealt to the threads: column pairs from ca,
+// npairs of them, nb row bands of R rows (nb * npairs <= NT).
+struct BandPlan {
+    int ca, npairs, nb, R;
+    float inv_np;  // ~1 / npairs (the band index, tile_step)
+};
+
+// The plan of region [c_lo, c_hi) x [r_lo, r_hi) (non-empty). With constant
+// arguments (a whole interior tile, every step after unrolling) it folds to
+// constants; the integer divisions then cost nothing -- they were ~60 of the
+// ~100 VALU instructions of a wave's per-step setup (profiles/heat_tile_r5.md).
+template <int NT>
+__device__ __forceinline__ BandPlan band_plan(int c_lo, int c_hi, int r_lo, int r_hi) {
+    BandPlan p;
+    p.ca = c_lo & ~1;
+    p.npairs = (c_hi - p.ca + 1) >> 1;
+    p.nb = NT / p.npairs;
+    p.nb = p.nb < 1 ? 1 : p.nb;
+    p.R = (r_hi - r_lo + p.nb - 1) / p.nb;
+    p.inv_np = __builtin_amdgcn_rcpf((float)p.npairs);
+    return p;
+}
+
 // One timestep of the tile: rows [r_lo, r_hi) x columns [c_lo, c_hi) (LDS
-// coordinates) from src into dst.
+// coordinates) from src into dst, dealt to the threads by plan `pl`.
 template <typename T, int ORDER, bool FMA, int PW, int NT>
 __device__ __forceinline__ void tile_step(const T* __restrict__ src, T* __restrict__ dst, int c_lo, int c_hi, int r_lo,
-                                          int r_hi, T xcfl, T ycfl) {
+                                          int r_hi, const BandPlan& pl, T xcfl, T ycfl) {
     if (c_hi <= c_lo || r_hi <= r_lo) return;
-    const int ca = c_lo & ~1;
-    const int npairs = (c_hi - ca + 1) >> 1;
-    int nb = NT / npairs;
-    nb = nb < 1 ? 1 : nb;
-    const int rows = r_hi - r_lo;
-    const int R = (rows + nb - 1) / nb;
+    const int ca = pl.ca, npairs = pl.npairs, nb = pl.nb, R = pl.R;
     // band = task / npairs through a float reciprocal (3 VALU instead of a
     // ~20-instruction integer division per thread and step): task < NT and
     // npairs <= 64, so (task + 0.5) / npairs sits >= 1/128 from an integer and
-    // the float error (< 2^-12 here) cannot cross it
+    // the float error (rcp: 1 ulp; < 2^-12 here) cannot cross it
     static_assert(NT <= 4096, "tile_step: the reciprocal band index needs task < 4096");
-    const float inv_np = 1.0f / (float)npairs;
+    const float inv_np = pl.inv_np;
     for (int task = threadIdx.x; task < npairs * nb; task += NT) {
         const int band = (int)(((float)task + 0.5f) * inv_np);
         const int c0 = ca + 2 * (task - band * npairs);
@@ -235,12 +253,21 @@ __global__ __launch_bounds__(NT) void heat_tile_kernel(const T* __restrict__ pre
     if (trace && threadIdx.x == 0) tr[1] = wall_clock64();
     // region g in LDS coordinates
     const int gxl = g.xb - gx0, gxh = g.xe - gx0, gyl = g.yb - gy0, gyh = g.ye - gy0;
+    // a tile whose every step region is unclipped by g (all but the edge
+    // tiles) takes each step's band plan as compile-time constants
+    const bool inner = gxl <= B && gxh >= H + TX + (NS - 1) * B && gyl <= B && gyh >= H + TY + (NS - 1) * B;
 #pragma unroll
     for (int s = 1; s <= NS; ++s) {
         const int e = (NS - s) * B;  // this step's reach beyond the output tile
         const int c_lo = max(H - e, gxl), c_hi = min(H + TX + e, gxh);
         const int r_lo = max(H - e, gyl), r_hi = min(H + TY + e, gyh);
-        tile_step<T, ORDER, FMA, PW, NT>((s & 1) ? L0 : L1, (s & 1) ? L1 : L0, c_lo, c_hi, r_lo, r_hi, xcfl, ycfl);
+        BandPlan pl{0, 1, 1, 1, 1.0f};
+        if (inner)
+            pl = band_plan<NT>(H - e, H + TX + e, H - e, H + TY + e);
+        else if (c_hi > c_lo && r_hi > r_lo)
+            pl = band_plan<NT>(c_lo, c_hi, r_lo, r_hi);
+        tile_step<T, ORDER, FMA, PW, NT>((s & 1) ? L0 : L1, (s & 1) ? L1 : L0, c_lo, c_hi, r_lo, r_hi, pl, xcfl,
+                                         ycfl);
         __syncthreads();
         if (trace && threadIdx.x == 0) tr[1 + s] = wall_clock64();
     }
