@@ -317,7 +317,7 @@ CME_EXPORT int cme_transpose_f32(const float* in, float* out, int rows, int cols
             } else if (variant == 8) {
                 return launch_vec_tile<64, 64, 1>(in, out, rows, cols, s);
             } else {
-                // benchmarks/tune_transpose.py (profiles/transpose_tune_r2.md):
+                // benchmarks/tune_transpose.py (profiles/transpose_tune_r2.log):
                 // square -> 64x64 tiles in diagonal order with non-temporal
                 // output stores (6.88 TB/s at 8192^2, 6.54 at 4096^2, 5.16 at
                 // 16384^2; round 1's plain stores: 5.35 / 6.39 / 4.92);
