@@ -8,9 +8,11 @@ on the device and every multiply is one HIP kernel (two for HYB).
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
+
 import torch
 
 from .. import _ext
@@ -327,6 +329,31 @@ def stream_rows(a: CSR) -> int:
     return 512 if mean <= 6 else (256 if mean <= 12 else (128 if mean <= 24 else 64))
 
 
+# CSR "auto" on short, regular rows (mean <= 8, longest <= 16 entries: the
+# 5-point Laplacian of config #4) takes csr_scalar: 13.5 / 11.4 us cold / warm
+# on the 1M matrix against 14.9 / 12.2 for CSR-stream; its lane-per-row loop
+# would serialise a long row, hence the bound on the longest
+# (profiles/spmv_stream_r5.md)
+SCALAR_MAX_MEAN, SCALAR_MAX_ROW = 8, 16
+# row-pointer tensor (by identity) -> (weak reference, longest row): one
+# device sync per matrix, then cached
+_MAX_ROW: dict = {}
+
+
+def max_row_length(a: CSR) -> int | None:
+    """Longest row of ``a`` (cached per row-pointer tensor; None while a
+    stream is being captured and the value is not cached yet)."""
+    hit = _MAX_ROW.get(id(a.rp))
+    if hit is not None and hit[0]() is a.rp:
+        return hit[1]
+    if a.rp.is_cuda and torch.cuda.is_current_stream_capturing():
+        return None
+    v = int(torch.diff(a.rp).max().item()) if a.nrows > 0 else 0
+    key = id(a.rp)
+    _MAX_ROW[key] = (weakref.ref(a.rp, lambda _r, k=key: _MAX_ROW.pop(k, None)), v)
+    return v
+
+
 # mean row length below which CSR "auto" takes the stream kernel (measured,
 # cold / MALL defeated, profiles/spmv_stream_r5.md: 27-pt Laplacian, 26.5 per
 # row, stream 1005 vs vector 415 GFLOP/s; random 16 per row 299 vs 248; skewed
@@ -346,8 +373,9 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
     """y = A x + beta*y for any of the formats. ``kernel`` (CSR only):
     "scalar", "vector", "stream" (CSR-stream: row blocks staged through LDS),
     "short" (a lane per row, the first 8 entries of a row as one batch of loads),
-    or "auto" (stream for a mean row length below 32, where CSR-vector idles
-    most of its lanes; vector with auto group above). To pick the FORMAT by
+    or "auto" (scalar for short regular rows -- mean <= 8, longest <= 16 --,
+    stream for a mean row length below 32, where CSR-vector idles most of its
+    lanes; vector with auto group above). To pick the FORMAT by
     the matrix structure, convert once with :func:`prepare`."""
     if y is None:
         nrows = a.ell.nrows if isinstance(a, HYB) else a.nrows
@@ -367,6 +395,10 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
         g = max(1, auto_group(a) // 4) if kernel != "scalar" else 1
         _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.nnz, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), g, float(beta), s)
+    elif isinstance(a, CSR) and kernel == "auto" and a.nnz <= SCALAR_MAX_MEAN * max(1, a.nrows) and \
+            (max_row_length(a) or SCALAR_MAX_ROW + 1) <= SCALAR_MAX_ROW:
+        _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
+                      y.data_ptr(), 1, float(beta), s)
     elif isinstance(a, CSR) and kernel == "short":
         _ext.call_hip("cme_spmv_csr_short", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), short_rows_per_lane(a), float(beta), s)

@@ -82,7 +82,7 @@ def bench_primitives(dev) -> dict:
     against ``x.t()``; my-refs/MatrixTranspose.pdf p.19), the 2^26 fp32 scan
     (decoupled look-back and Blelloch) and reduction against a float64 torch
     reference (my-refs/scan.pdf p.16 Table 2), and SpMV on the 1M-row 5-point
-    Laplacian in CSR (``auto``: the CSR-stream kernel) and ELL with the
+    Laplacian in CSR (``auto``: lane-per-row for its short regular rows) and ELL with the
     256 MB Infinity Cache defeated (operand copies >= 768 MB visited
     round-robin; refs/Bell SC 2009.pdf §4.2), against a float64 reference.
     Each figure is the median of event-timed batches of back-to-back calls

@@ -188,6 +188,20 @@ def test_spmv_csr_stream_blocks(gpu, rows_case, kernel, rpt):
     assert stream_rows(a) in (64, 128, 256, 512)
 
 
+def test_csr_auto_scalar_rule():
+    """CSR "auto" takes the lane-per-row kernel for short regular rows only:
+    mean <= 8 and no row longer than 16 (one long row would serialise its
+    lane); the longest row is cached per row-pointer tensor."""
+    from cme213x.ops.spmv import SCALAR_MAX_MEAN, SCALAR_MAX_ROW, max_row_length
+
+    assert (SCALAR_MAX_MEAN, SCALAR_MAX_ROW) == (8, 16)
+    a = laplacian("5pt", 50)
+    assert max_row_length(a) == 5 and max_row_length(a) == 5
+    rp = torch.tensor([0, 2, 40, 41], dtype=torch.int32)
+    b = CSR(3, 50, rp, torch.zeros(41, dtype=torch.int32), torch.ones(41))
+    assert max_row_length(b) == 38
+
+
 def test_csr_auto_kernel_rule():
     """CSR "auto" takes the stream kernel below a mean of 32 nonzeros per row
     (rows per block from the mean), the vector kernel above."""
