@@ -49,6 +49,7 @@
 // behind; the compiler emitted none, and waves then ran the previous ticket
 // (two tasks wrong in ~1 run of 5 at 4096^2).
 #include "heat_pipe.h"
+#include "cme213/persist_ws.h"
 
 using namespace cme;
 
@@ -216,37 +217,14 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
     }
 }
 
-// per-call control words + completion words, zeroed by one memset node; the
-// block starts at its allocation and is padded to 16 B
-struct FlowWs {
-    unsigned* dev = nullptr;
-    size_t words = 0;
-    unsigned* timeout = nullptr;  // pinned
-};
-FlowWs& flow_ws() {
-    static FlowWs w;
+// per-call control words + completion words + give-up records
+// (cme213/persist_ws.h), zeroed by one memset node
+PersistWs& flow_ws() {
+    static PersistWs w;
     return w;
 }
 
 constexpr size_t kCtlWords = kCtlStride * (kBands + 1);
-
-int flow_prepare(size_t done_words, FlowWs** out) {
-    FlowWs& w = flow_ws();
-    const size_t need = ((kCtlWords + done_words + 16 * 64 + 3) / 4) * 4;  // + 64 give-up records
-    if (w.words < need) {
-        if (w.dev) CME_TRY(hipFree(w.dev));
-        w.dev = nullptr;
-        w.words = 0;
-        CME_TRY(hipMalloc(&w.dev, need * 4));
-        w.words = need;
-    }
-    if (!w.timeout) {
-        CME_TRY(hipHostMalloc(&w.timeout, 16, hipHostMallocCoherent));
-        *w.timeout = 0u;
-    }
-    *out = &w;
-    return 0;
-}
 
 template <typename T, int ORDER, int NS, int FMA, int RB, int PD, bool NT, int WPR, int VW, int OCC, int OST>
 int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npass, hipStream_t s,
@@ -287,9 +265,9 @@ int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npa
     const int nch = (int)cdiv(H, chunk);
     const long tpp = (long)strips * nch;
     if (tpp * npass >= (1l << 31) || chunk >= 65536) return (int)hipErrorInvalidValue;
-    FlowWs* w = nullptr;
+    PersistWs* w = &flow_ws();
     {
-        const int rc = flow_prepare((size_t)tpp, &w);
+        const int rc = w->reserve(kCtlWords + (size_t)tpp + 16 * 64);  // + 64 give-up records
         if (rc) return rc;
     }
     CME_TRY(hipMemsetAsync(w->dev, 0, w->words * 4, s));
@@ -375,7 +353,7 @@ CME_EXPORT int cme_heat_flow_trace_f32(float* a, float* b, int pitch, int gy, in
 // 32 (x + 1), completion words from word 288, then the give-up records) to
 // host memory (synchronous).
 CME_EXPORT int cme_heat_flow_debug(unsigned* host, int nwords) {
-    FlowWs& w = flow_ws();
+    PersistWs& w = flow_ws();
     if (!w.dev || nwords < 0) return (int)hipErrorInvalidValue;
     if ((size_t)nwords > w.words) nwords = (int)w.words;
     return (int)hipMemcpy(host, w.dev, (size_t)nwords * 4, hipMemcpyDeviceToHost);
@@ -384,9 +362,7 @@ CME_EXPORT int cme_heat_flow_debug(unsigned* host, int nwords) {
 // Sticky give-up flag of the flow launches (pinned host word; read after the
 // stream is synchronised). reset != 0 clears it.
 CME_EXPORT int cme_heat_flow_status(unsigned* timed_out, int reset) {
-    FlowWs& w = flow_ws();
-    *timed_out = w.timeout ? *w.timeout : 0u;
-    if (reset && w.timeout) *w.timeout = 0u;
+    *timed_out = flow_ws().take_timeout(reset != 0);
     return 0;
 }
 

@@ -46,6 +46,7 @@
 // cme_heat_tile_res_status. The launch is cooperative, so a grid that cannot
 // be co-resident is refused at launch instead of deadlocking.
 #include "heat_tile.h"
+#include "cme213/persist_ws.h"
 #include "cme213/tuning.h"
 
 using namespace cme;
@@ -301,13 +302,8 @@ __global__ __launch_bounds__(NT) void heat_tile_res_kernel(T* a, T* b, int pitch
     }
 }
 
-struct ResWs {
-    unsigned* dev = nullptr;
-    size_t words = 0;
-    unsigned* timeout = nullptr;  // pinned
-};
-ResWs& res_ws() {
-    static ResWs w;
+PersistWs& res_ws() {  // abort word + completion words (cme213/persist_ws.h)
+    static PersistWs w;
     return w;
 }
 
@@ -337,18 +333,11 @@ int launch_res(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npas
         return (long)per_cu * device_cu_count();
     }();
     if (ntiles > resident) return (int)hipErrorCooperativeLaunchTooLarge;  // the caller runs tile passes
-    ResWs& w = res_ws();
-    const size_t need = ((kCtlWords + (size_t)ntiles + 3) / 4) * 4;
-    if (w.words < need) {
-        if (w.dev) CME_TRY(hipFree(w.dev));
-        w.dev = nullptr;
-        w.words = 0;
-        CME_TRY(hipMalloc(&w.dev, need * 4));
-        w.words = need;
-    }
-    if (!w.timeout) {
-        CME_TRY(hipHostMalloc(&w.timeout, 16, hipHostMallocCoherent));
-        *w.timeout = 0u;
+    PersistWs& w = res_ws();
+    const size_t need = kCtlWords + (size_t)ntiles;
+    {
+        const int rc = w.reserve(need);
+        if (rc) return rc;
     }
     CME_TRY(hipMemsetAsync(w.dev, 0, need * 4, s));
     ResArgs f;
@@ -423,9 +412,7 @@ CME_EXPORT int cme_heat_tile_res_f32(float* a, float* b, int pitch, int gy, int 
 // Sticky give-up flag of the resident launches (pinned host word; read after
 // the stream is synchronised). reset != 0 clears it.
 CME_EXPORT int cme_heat_tile_res_status(unsigned* timed_out, int reset) {
-    ResWs& w = res_ws();
-    *timed_out = w.timeout ? *w.timeout : 0u;
-    if (reset && w.timeout) *w.timeout = 0u;
+    *timed_out = res_ws().take_timeout(reset != 0);
     return 0;
 }
 
