@@ -335,8 +335,9 @@ def stream_rows(a: CSR) -> int:
 # would serialise a long row, hence the bound on the longest
 # (profiles/spmv_stream_r5.md)
 SCALAR_MAX_MEAN, SCALAR_MAX_ROW = 8, 16
-# row-pointer tensor (by identity) -> (weak reference, longest row): one
-# device sync per matrix, then cached
+# row-pointer tensor (by identity) -> (weak reference, version, longest row):
+# one device sync per matrix, then cached; an in-place write to the row
+# pointers bumps the tensor's version and invalidates the entry
 _MAX_ROW: dict = {}
 
 
@@ -344,13 +345,13 @@ def max_row_length(a: CSR) -> int | None:
     """Longest row of ``a`` (cached per row-pointer tensor; None while a
     stream is being captured and the value is not cached yet)."""
     hit = _MAX_ROW.get(id(a.rp))
-    if hit is not None and hit[0]() is a.rp:
-        return hit[1]
+    if hit is not None and hit[0]() is a.rp and hit[1] == a.rp._version:
+        return hit[2]
     if a.rp.is_cuda and torch.cuda.is_current_stream_capturing():
         return None
     v = int(torch.diff(a.rp).max().item()) if a.nrows > 0 else 0
     key = id(a.rp)
-    _MAX_ROW[key] = (weakref.ref(a.rp, lambda _r, k=key: _MAX_ROW.pop(k, None)), v)
+    _MAX_ROW[key] = (weakref.ref(a.rp, lambda _r, k=key: _MAX_ROW.pop(k, None)), a.rp._version, v)
     return v
 
 

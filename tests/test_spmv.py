@@ -200,6 +200,8 @@ def test_csr_auto_scalar_rule():
     rp = torch.tensor([0, 2, 40, 41], dtype=torch.int32)
     b = CSR(3, 50, rp, torch.zeros(41, dtype=torch.int32), torch.ones(41))
     assert max_row_length(b) == 38
+    rp[1:] = torch.tensor([20, 40, 41], dtype=torch.int32)  # in-place edit: the cached value is dropped
+    assert max_row_length(b) == 20
 
 
 def test_csr_auto_kernel_rule():
