@@ -24,6 +24,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_radix_onesweep", "ppppppqiiipqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_radix_lane_order", "i")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_u32", "ppppqp")
 _ext.proto(_ext.HIP_PROTOS, "cme_merge_sort", "ppppppqip")
+_ext.proto(_ext.HIP_PROTOS, "cme_merge_sort_ws", "ppppppqipp")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_u32", "ppqii")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_radix_sort_serial_u32", "ppqi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_merge_sort_i32", "ppqqqp")
@@ -98,9 +99,11 @@ def radix_lane_order(check: bool = True) -> bool:
 
 
 def _merge(keys: torch.Tensor, values: torch.Tensor | None):
-    """GPU merge sort (csrc/hip/sort.hip cme_merge_sort): stable; 4096-key
+    """GPU merge sort (csrc/hip/sort.hip cme_merge_sort_ws): stable; 8192-key
     block sorts, then one LDS-staged merge-path pass per doubling of the run
-    length; key transforms fused into the first and last kernels."""
+    length; from 8M keys each pass first finds every tile's merge-path split
+    in one launch (tuning knob merge_part), below that each merge block
+    searches its own; key transforms fused into the first and last kernels."""
     if keys.dtype not in _MODES:
         raise TypeError(f"unsupported key dtype {keys.dtype}")
     k = keys.contiguous()
@@ -112,8 +115,9 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
         v = values.contiguous()
         vout, vtmp = torch.empty_like(v), torch.empty_like(v)
         vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
-    _ext.call_hip("cme_merge_sort", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
-                  _MODES[keys.dtype], _ext.stream_ptr(keys.device))
+    ws = _workspace(keys.device, (k.numel() + 4095) // 4096 * 8 + 256)  # = cme_merge_ws_bytes
+    _ext.call_hip("cme_merge_sort_ws", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
+                  _MODES[keys.dtype], ws.data_ptr(), _ext.stream_ptr(keys.device))
     return (out, vout) if values is not None else out
 
 

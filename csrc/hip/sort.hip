@@ -402,7 +402,9 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
 //                (stable), then 9 rounds of merge path in LDS (runs of 16 ->
 //                8192, A first on ties: stable; LDS padded one word per 16);
 //   merge pass : output tile o (4096 keys) of a pass merging runs of L: the
-//                block finds its two diagonal splits by a cooperative 128-ary
+//                block takes its two diagonal splits from the pass's
+//                partition launch (ms_partition_kernel, 8 lanes per tile;
+//                from 8M keys) or finds them by a cooperative 128-ary
 //                search (2 x 128 lanes, ~4 dependent rounds of global loads
 //                instead of ~24), loads the A and B pieces into LDS with
 //                coalesced loads, merges 16 outputs per lane from LDS and
@@ -579,38 +581,93 @@ __device__ __forceinline__ long long ms_coop_split(const uint32_t* __restrict__ 
     return lo;
 }
 
-template <bool HAS_VALUES>
-__global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_t* __restrict__ ki,
-                                                                   uint32_t* __restrict__ ko,
-                                                                   const uint32_t* __restrict__ vi,
-                                                                   uint32_t* __restrict__ vo, long long n,
-                                                                   long long L, int mode_out) {
-    __shared__ uint32_t sk[lp_size(kMsTile)];
-    __shared__ uint32_t sv[HAS_VALUES ? lp_size(kMsTile) : 1];
+// Merge-path partitions of a whole pass, G lanes per output tile: split[t]
+// = the number of A keys among the first (t * tile - a0) outputs of tile
+// t's pair, by a G-ary search (one load pair per lane and round, ~log_G L
+// dependent rounds, no barrier). All tiles' searches run at once here, so the
+// merge kernel's blocks start on their loads instead of each paying the
+// search's dependent global rounds on its own critical path. G trades rounds
+// (latency) against the lines each round touches (G per array and tile).
+template <int G>
+__global__ __launch_bounds__(256) void ms_partition_kernel(const uint32_t* __restrict__ ki, long long n, long long L,
+                                                           long long tile, long long ntiles,
+                                                           long long* __restrict__ split) {
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "partition group: 4-64 lanes");
+    const long long t = ((long long)blockIdx.x * 256 + threadIdx.x) / G;
+    const int sub = threadIdx.x % G;
+    const int gshift = lane_id() & ~(G - 1);  // the group's first lane in the wave
+    const uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1);
+    const bool valid = t < ntiles;
+    const long long o0 = valid ? t * tile : 0;
+    const long long a0 = o0 & ~(2 * L - 1);
+    const long long la = a0 + L < n ? L : n - a0;
+    const long long lb = a0 + 2 * L < n ? L : (n - a0 - la > 0 ? n - a0 - la : 0);
+    const uint32_t* A = ki + a0;
+    const uint32_t* B = ki + a0 + la;
+    const long long diag = o0 - a0;
+    long long lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
+    while (__ballot(lo < hi)) {  // until every group of the wave is done
+        const bool act = lo < hi;
+        const long long step = (hi - lo + G - 1) / G;
+        const long long m = lo + (long long)sub * step;
+        const bool q = act && m < hi && A[m] <= B[diag - 1 - m];
+        const uint64_t fails = (__ballot(!q) >> gshift) & gmask;
+        const int f = fails ? __builtin_ctzll(fails) : G;
+        if (act) {
+            const long long nlo = f == 0 ? lo : lo + (long long)(f - 1) * step + 1;
+            const long long mf = lo + (long long)f * step;
+            hi = f == G ? hi : (mf < hi ? mf : hi);
+            lo = nlo;
+        }
+    }
+    if (valid && sub == 0) split[t] = lo;
+}
+
+// split: the pass's partitions from ms_partition_kernel, or nullptr for the
+// in-block cooperative search (NT = 256 only). NT lanes merge an output tile
+// of NT * 16 keys.
+template <bool HAS_VALUES, int NT = kMsThreads>
+__global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko,
+                                                           const uint32_t* __restrict__ vi, uint32_t* __restrict__ vo,
+                                                           long long n, long long L, int mode_out,
+                                                           const long long* __restrict__ split) {
+    constexpr int TILE = NT * kMsItems;
+    __shared__ uint32_t sk[lp_size(TILE)];
+    __shared__ uint32_t sv[HAS_VALUES ? lp_size(TILE) : 1];
     __shared__ uint64_t smask[2][2];
     __shared__ long long ssplit[2];
     const int t = threadIdx.x;
     // consecutive output tiles on one XCD: their diagonal searches probe the
     // same lines of A and B, which then hit that XCD's L2
-    const long long o0 = (long long)xcd_remap(blockIdx.x, gridDim.x) * kMsTile;
-    const long long o1 = o0 + kMsTile < n ? o0 + kMsTile : n;
+    const long long tile = xcd_remap(blockIdx.x, gridDim.x);
+    const long long o0 = tile * TILE;
+    const long long o1 = o0 + TILE < n ? o0 + TILE : n;
     const long long a0 = o0 & ~(2 * L - 1);  // pair start (2L is a multiple of the tile)
     const long long la = a0 + L < n ? L : n - a0;
     const long long lb = a0 + 2 * L < n ? L : (n - a0 - la > 0 ? n - a0 - la : 0);
     const uint32_t* A = ki + a0;
     const uint32_t* B = ki + a0 + la;
-    const int part = t >> 7;
-    const long long diag = (part == 0 ? o0 : o1) - a0;
-    int rounds = 0;  // ceil(log_128(L + 1)): candidates per search <= L + 1
-    for (long long w = L + 1; w > 1; w = (w + 127) / 128) ++rounds;
-    const long long sp = ms_coop_split(A, B, la, lb, diag, rounds, smask);
-    if ((t & 127) == 0) ssplit[part] = sp;
-    __syncthreads();
-    const long long i0 = ssplit[0], i1 = ssplit[1];
+    long long i0, i1;
+    if (split) {  // block-uniform
+        i0 = split[tile];
+        i1 = o1 - a0 == la + lb ? la : split[tile + 1];  // a tile ending its pair took all of A
+    } else if constexpr (NT == 256) {
+        const int part = t >> 7;
+        const long long diag = (part == 0 ? o0 : o1) - a0;
+        int rounds = 0;  // ceil(log_128(L + 1)): candidates per search <= L + 1
+        for (long long w = L + 1; w > 1; w = (w + 127) / 128) ++rounds;
+        const long long sp = ms_coop_split(A, B, la, lb, diag, rounds, smask);
+        if ((t & 127) == 0) ssplit[part] = sp;
+        __syncthreads();
+        i0 = ssplit[0];
+        i1 = ssplit[1];
+    } else {
+        i0 = i1 = 0;  // the host never launches this
+    }
     const long long j0 = (o0 - a0) - i0, j1 = (o1 - a0) - i1;
     int na = (int)(i1 - i0), nb = (int)(j1 - j0);
-    if (na < 0 || nb < 0 || na + nb > kMsTile || i1 > la || j1 > lb) na = nb = 0;  // never out of range
-    for (int x = t; x < na + nb; x += kMsThreads) {
+    if (na < 0 || nb < 0 || na + nb > TILE || i1 > la || j1 > lb) na = nb = 0;  // never out of range
+    for (int x = t; x < na + nb; x += NT) {
         const bool ia = x < na;
         const long long g = ia ? a0 + i0 + x : a0 + la + j0 + (x - na);
         sk[lp(x)] = ki[g];
@@ -621,8 +678,8 @@ __global__ __launch_bounds__(kMsThreads) void ms_merge_pass_kernel(const uint32_
     const int diag_l = kMsItems * t < cnt ? kMsItems * t : cnt;
     const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int x) { return sk[lp(na + x)]; }, na, nb, diag_l);
     uint32_t k[kMsItems], v[kMsItems];
-    ms_merge16<HAS_VALUES, kMsTile>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
-    ms_store_tile<HAS_VALUES, kMsThreads>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
+    ms_merge16<HAS_VALUES, TILE>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
+    ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
 }
 
 }  // namespace
@@ -825,8 +882,19 @@ CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
 // Stable merge sort of n keys from `in` into `out` (ping-pong through `tmp`;
 // `in` may equal `out`; values optional, likewise). mode: 0 uint32, 1 int32,
 // 2 float32 keys.
-CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
-                              uint32_t* vtmp, long long n, int mode, void* stream) {
+CME_EXPORT long long cme_merge_ws_bytes(long long n) { return (long long)cdiv(n, kMsTile) * 8 + 256; }
+
+// merge-pass output tile (tuning knob merge_tile: 4096 or 8192 keys; 8192
+// needs the partition launch)
+static int merge_tile(bool part) {
+    return part && cme::tune_get(cme::kTuneMergeTile) == 8192 ? 8192 : kMsTile;
+}
+
+// ws (cme_merge_ws_bytes(n) bytes, or nullptr): with it every merge pass
+// first computes all tile partitions in one launch (ms_partition_kernel);
+// without it each merge block searches its own (ms_coop_split).
+CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin,
+                                 uint32_t* vout, uint32_t* vtmp, long long n, int mode, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
     if (n <= 0) return 0;
     if (mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) || (vin && !vtmp))
@@ -836,7 +904,15 @@ CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     // the block sort writes where an even number of passes later lands in out
     uint32_t* d0 = (npass & 1) ? tmp : out;
     uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
-    const unsigned btiles = cdiv(n, kBsTile), tiles = cdiv(n, kMsTile);
+    // partitions: tuning knob merge_part (G lanes per tile, 0 = in-block
+    // searches, -1 = auto: G = 8 from 8M keys). Measured (profiles/sort_r5.md):
+    // 48M int32 2.21 -> 1.59 ms, 16M 0.65 -> 0.55; at 1M and 4M the extra
+    // launch per pass costs more than the searches it moves (1M 0.124 ->
+    // 0.136 ms, 4M 0.222 -> 0.230).
+    long part = ws ? cme::tune_get(cme::kTuneMergePart) : 0;
+    if (part < 0) part = n >= (8ll << 20) ? 8 : 0;
+    const int mtile = merge_tile(part != 0);
+    const unsigned btiles = cdiv(n, kBsTile), tiles = cdiv(n, mtile);
     if (vin)
         hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode,
                            npass ? 0 : mode);
@@ -850,17 +926,45 @@ CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         const bool last = p == npass - 1;
         uint32_t* ko = (ki == out) ? tmp : out;
         uint32_t* vo = vin ? ((vi == vout) ? vtmp : vout) : nullptr;
-        if (vin)
+        long long* split = part ? (long long*)ws : nullptr;
+        if (split) {
+            const int g = part == 4 || part == 8 || part == 16 || part == 32 ? (int)part : 64;
+            const dim3 grid(cdiv((long long)tiles * g, 256));
+#define CME_PART(G)                                                                                               \
+    hipLaunchKernelGGL(ms_partition_kernel<G>, grid, dim3(256), 0, s, ki, n, L, (long long)mtile, (long long)tiles, \
+                       split)
+            if (g == 4) CME_PART(4);
+            else if (g == 8) CME_PART(8);
+            else if (g == 16) CME_PART(16);
+            else if (g == 32) CME_PART(32);
+            else CME_PART(64);
+#undef CME_PART
+        }
+        const int mo = last ? mode : 0;
+        if (mtile == 8192) {
+            if (vin)
+                hipLaunchKernelGGL((ms_merge_pass_kernel<true, 512>), dim3(tiles), dim3(512), 0, s, ki, ko, vi, vo, n,
+                                   L, mo, split);
+            else
+                hipLaunchKernelGGL((ms_merge_pass_kernel<false, 512>), dim3(tiles), dim3(512), 0, s, ki, ko, vi, vo, n,
+                                   L, mo, split);
+        } else if (vin) {
             hipLaunchKernelGGL(ms_merge_pass_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n, L,
-                               last ? mode : 0);
-        else
-            hipLaunchKernelGGL(ms_merge_pass_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n,
-                               L, last ? mode : 0);
+                               mo, split);
+        } else {
+            hipLaunchKernelGGL(ms_merge_pass_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n, L,
+                               mo, split);
+        }
         CME_TRY(hipGetLastError());
         ki = ko;
         vi = vo;
     }
     return 0;
+}
+
+CME_EXPORT int cme_merge_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin, uint32_t* vout,
+                              uint32_t* vtmp, long long n, int mode, void* stream) {
+    return cme_merge_sort_ws(in, out, tmp, vin, vout, vtmp, n, mode, nullptr, stream);
 }
 
 // In-place form (keys sorted into `keys`; keys_alt / vals_alt scratch).

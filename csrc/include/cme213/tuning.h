@@ -44,6 +44,8 @@ enum TuneKey : int {
     kTuneTileResNs,        // CME_TILE_RES_NS: steps per halo exchange of the resident tiles (2 or 4)
     kTuneTileResMinR,      // CME_TILE_RES_MINR: rows per band at least in the resident tiles' steps
     kTuneSpmvShortRpt,     // CME_SPMV_SHORT_RPT: CSR-short rows per lane (1, 2, 4)
+    kTuneMergePart,        // CME_MERGE_PART: merge sort partitions: 4 / 8 / 16 / 32 / 64 lanes per tile in one search launch per pass (other positive: 64), 0 in-block searches, -1 auto (8 from 8M keys)
+    kTuneMergeTile,        // CME_MERGE_TILE: merge sort output tile per merge-pass block, 4096 or 8192 keys (8192 with partitions)
     kTuneCount
 };
 

@@ -172,6 +172,29 @@ def test_merge_sort_skewed_and_stable(gpu, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("part,tile", [(-1, 4096), (0, 4096), (4, 4096), (8, 4096), (16, 4096), (64, 4096), (8, 8192), (64, 8192)])
+def test_merge_sort_partition_arms(gpu, part, tile):
+    """Every way a merge pass finds its tile splits (tuning knob merge_part:
+    G = 4 / 8 / 16 / 64 lanes per tile in one partition launch per pass; 0 each
+    block's cooperative search; -1 the size rule) and both merge tiles (merge_tile) sort keys
+    and key-value pairs stably, across pair ends, a last run without a
+    partner and passes of several search rounds."""
+    from cme213x.utils import tuning
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    with tuning.override(merge_part=part, merge_tile=tile):
+        for n in (8193, 3 * 8192 + 4095, 1 << 20, 9 * (1 << 20) + 5):
+            k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+            k[n // 2:] = k[n // 2:] % 11  # long runs of equal keys: ties across the split diagonals
+            v = torch.arange(n, device="cuda", dtype=torch.int32)
+            ks, vs = sort(k, values=v, algo="merge")
+            rk, ri = torch.sort(k.cpu().long(), stable=True)
+            assert torch.equal(ks.cpu().long(), rk), n
+            assert torch.equal(vs.cpu().long(), ri), n
+            assert torch.equal(sort(k, algo="merge").cpu().long(), rk), n
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("arm", [0, 1, 2, 3, 4, 5, 7, 8, 10, 14])
 def test_radix_downsweep_arms(gpu, arm):
     """Every reduce-then-scan downsweep arm (tuning knob radix_ds: atomic
