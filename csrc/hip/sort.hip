@@ -448,26 +448,35 @@ __device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
 }
 
 // sequential merge of kMsItems outputs from A = [a0, a0+la) / B = [b0, b0+lb)
-// (logical LDS indices, padded on access) into registers
+// (logical LDS indices, padded on access) into registers. Branch-free: every
+// step selects its output, advances one of the two cursors and loads that
+// run's next key (the load address is always inside the buffer: CAP + 1
+// padded slots), so no lane diverges -- the divergent form spent more issue
+// slots on exec-mask bookkeeping than on the merge.
 template <bool HAS_VALUES, int CAP>
 __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* sv, int a0, int la, int b0, int lb,
                                            int i, int j, uint32_t (&k)[kMsItems], uint32_t (&v)[kMsItems]) {
-    uint32_t ka = i < la ? sk[lp(a0 + i)] : 0xffffffffu, kb = j < lb ? sk[lp(b0 + j)] : 0xffffffffu;
+    int pa = a0 + i, pb = b0 + j;  // cursors (logical indices)
+    const int ea = a0 + la, eb = b0 + lb;
+    uint32_t ka = sk[lp(pa < ea ? pa : CAP)], kb = sk[lp(pb < eb ? pb : CAP)];
+    ka = pa < ea ? ka : 0xffffffffu;
+    kb = pb < eb ? kb : 0xffffffffu;
 #pragma unroll
     for (int q = 0; q < kMsItems; ++q) {
-        const bool take_a = j >= lb || (i < la && ka <= kb);
+        const bool take_a = pb >= eb || (pa < ea && ka <= kb);
         k[q] = take_a ? ka : kb;
         if constexpr (HAS_VALUES) {
-            const int x = take_a ? a0 + i : b0 + j;  // past both ends only on padding lanes
+            const int x = take_a ? pa : pb;  // past both ends only on padding lanes
             v[q] = sv[lp(x < CAP ? x : CAP - 1)];
         }
-        if (take_a) {
-            ++i;
-            ka = i < la ? sk[lp(a0 + i)] : 0xffffffffu;
-        } else {
-            ++j;
-            kb = j < lb ? sk[lp(b0 + j)] : 0xffffffffu;
-        }
+        pa += take_a ? 1 : 0;
+        pb += take_a ? 0 : 1;
+        const int np = take_a ? pa : pb;
+        const int ne = take_a ? ea : eb;
+        uint32_t nv = sk[lp(np < CAP ? np : CAP)];
+        nv = np < ne ? nv : 0xffffffffu;
+        ka = take_a ? nv : ka;
+        kb = take_a ? kb : nv;
     }
 }
 
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_
                                                                    const uint32_t* __restrict__ vi,
                                                                    uint32_t* __restrict__ vo, long long n,
                                                                    int mode_in, int mode_out) {
-    __shared__ uint32_t sk[lp_size(kBsTile)];
+    __shared__ uint32_t sk[lp_size(kBsTile) + 1];  // + the merge's out-of-run load slot
     __shared__ uint32_t sv[HAS_VALUES ? lp_size(kBsTile) : 1];
     const int t = threadIdx.x;
     const long long base = (long long)blockIdx.x * kBsTile;
@@ -519,15 +528,19 @@ __global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_
     for (int r = 0; r < kMsItems; ++r) {
 #pragma unroll
         for (int q = r & 1; q + 1 < kMsItems; q += 2) {
-            if (k[q] > k[q + 1]) {
-                const uint32_t x = k[q];
-                k[q] = k[q + 1];
-                k[q + 1] = x;
-                if constexpr (HAS_VALUES) {
+            if constexpr (HAS_VALUES) {
+                if (k[q] > k[q + 1]) {
+                    const uint32_t x = k[q];
+                    k[q] = k[q + 1];
+                    k[q + 1] = x;
                     const uint32_t y = v[q];
                     v[q] = v[q + 1];
                     v[q + 1] = y;
                 }
+            } else {  // equal keys are indistinguishable: min / max, no compare-select
+                const uint32_t lo = min(k[q], k[q + 1]), hi = max(k[q], k[q + 1]);
+                k[q] = lo;
+                k[q + 1] = hi;
             }
         }
     }
@@ -632,7 +645,7 @@ __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __res
                                                            long long n, long long L, int mode_out,
                                                            const long long* __restrict__ split) {
     constexpr int TILE = NT * kMsItems;
-    __shared__ uint32_t sk[lp_size(TILE)];
+    __shared__ uint32_t sk[lp_size(TILE) + 1];  // + the merge's out-of-run load slot
     __shared__ uint32_t sv[HAS_VALUES ? lp_size(TILE) : 1];
     __shared__ uint64_t smask[2][2];
     __shared__ long long ssplit[2];
