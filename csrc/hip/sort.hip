@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t rx_key_out(uint32_t u, int mode) {
     return u;
 }
 
-template <int UNR>
+template <int UNR, bool kUpVecCheck = true>
 __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint32_t* __restrict__ keys, long long n,
                                                                      long long chunk, int shift, int nblocks,
                                                                      uint32_t* __restrict__ counts, int mode) {
@@ -78,6 +78,29 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
             atomicAdd(&hist[d], 1u);
         }
     };
+    // the four keys of a 16-B load: ONE uniformity check for all of them (the
+    // wave's 256 consecutive keys), then either one atomic or four plain ones
+    auto add4 = [&](uint4 v) {
+        if (!kUpVecCheck) {
+            add(v.x);
+            add(v.y);
+            add(v.z);
+            add(v.w);
+            return;
+        }
+        const uint32_t dx = digit_of(rx_key_in(v.x, mode), shift), dy = digit_of(rx_key_in(v.y, mode), shift);
+        const uint32_t dz = digit_of(rx_key_in(v.z, mode), shift), dw = digit_of(rx_key_in(v.w, mode), shift);
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)dx);
+        if (__ballot((dx ^ d0) | (dy ^ d0) | (dz ^ d0) | (dw ^ d0)) == 0) {
+            const uint64_t act = __ballot(true);
+            if (lane == (int)__builtin_ctzll(act)) atomicAdd(&hist[d0], 4u * (uint32_t)__builtin_popcountll(act));
+        } else {
+            atomicAdd(&hist[dx], 1u);
+            atomicAdd(&hist[dy], 1u);
+            atomicAdd(&hist[dz], 1u);
+            atomicAdd(&hist[dw], 1u);
+        }
+    };
     // UNR 16-B loads in flight per lane before their LDS atomics (one load at
     // a time left the kernel waiting on HBM latency: wait-any 0.85 of its
     // cycles, profiles/sort_r3.md); tuning knob radix_up_unr
@@ -89,21 +112,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_upsweep_kernel(const uint3
 #pragma unroll
             for (int u = 0; u < UNR; ++u) v[u] = *reinterpret_cast<const uint4*>(keys + i + u * STEP);
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) {
-                add(v[u].x);
-                add(v[u].y);
-                add(v[u].z);
-                add(v[u].w);
-            }
+            for (int u = 0; u < UNR; ++u) add4(v[u]);
         }
     }
     for (; i < b1; i += STEP) {
         if (vec && i + 3 < b1) {
-            const uint4 v = *reinterpret_cast<const uint4*>(keys + i);
-            add(v.x);
-            add(v.y);
-            add(v.z);
-            add(v.w);
+            add4(*reinterpret_cast<const uint4*>(keys + i));
         } else {
             for (long long j = i; j < b1 && j < i + 4; ++j) add(keys[j]);
         }
@@ -818,7 +832,7 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     uint32_t* counts = (uint32_t*)ws;
     uint32_t* totals = counts + (size_t)nb * kBins;
     const int npass = (bit1 - bit0 + kRadixBits - 1) / kRadixBits;
-    const int up_unr = (int)cme::tune_get(cme::kTuneRadixUpUnr);  // upsweep 16-B loads in flight per lane: 4, 8, 16
+    const int up_unr = (int)cme::tune_get(cme::kTuneRadixUpUnr);  // upsweep 16-B loads in flight per lane: 4, 8, 16 (-4: per-key checks)
     const uint32_t* ki = in;
     const uint32_t* vi = vin;
     for (int p = 0; p < npass; ++p) {
@@ -835,6 +849,10 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         break;
             CME_UP(8) CME_UP(16)
 #undef CME_UP
+            case -4:  // the round-4 upsweep: a uniformity check per key instead of per 16-B load
+                hipLaunchKernelGGL((radix_upsweep_kernel<4, false>), dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk,
+                                   shift, nb, counts, mi);
+                break;
             default:
                 hipLaunchKernelGGL(radix_upsweep_kernel<4>, dim3(nb), dim3(kSortThreads), 0, s, ki, n, chunk, shift,
                                    nb, counts, mi);
