@@ -513,19 +513,18 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
     }
 }
 
-template <bool HAS_VALUES>
-__global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_t* __restrict__ ki,
-                                                                   uint32_t* __restrict__ ko,
-                                                                   const uint32_t* __restrict__ vi,
-                                                                   uint32_t* __restrict__ vo, long long n,
-                                                                   int mode_in, int mode_out) {
-    __shared__ uint32_t sk[lp_size(kBsTile) + 1];  // + the merge's out-of-run load slot
-    __shared__ uint32_t sv[HAS_VALUES ? lp_size(kBsTile) : 1];
+template <bool HAS_VALUES, int BS = kBsThreads>
+__global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko,
+                                                           const uint32_t* __restrict__ vi, uint32_t* __restrict__ vo,
+                                                           long long n, int mode_in, int mode_out) {
+    constexpr int BTILE = BS * kMsItems;
+    __shared__ uint32_t sk[lp_size(BTILE) + 1];  // + the merge's out-of-run load slot
+    __shared__ uint32_t sv[HAS_VALUES ? lp_size(BTILE) : 1];
     const int t = threadIdx.x;
-    const long long base = (long long)blockIdx.x * kBsTile;
-    const int cnt = (int)(n - base < kBsTile ? n - base : kBsTile);
+    const long long base = (long long)blockIdx.x * BTILE;
+    const int cnt = (int)(n - base < BTILE ? n - base : BTILE);
     // coalesced load into LDS, then lane t takes keys [16t, 16t+16)
-    for (int i = t; i < kBsTile; i += kBsThreads) {
+    for (int i = t; i < BTILE; i += BS) {
         sk[lp(i)] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
         if constexpr (HAS_VALUES) sv[lp(i)] = i < cnt ? vi[base + i] : 0u;
     }
@@ -559,7 +558,7 @@ __global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_
         }
     }
     // merge rounds in LDS: runs of 16 << r
-    for (int L = kMsItems; L < kBsTile; L <<= 1) {
+    for (int L = kMsItems; L < BTILE; L <<= 1) {
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kMsItems; ++q) {
@@ -572,9 +571,9 @@ __global__ __launch_bounds__(kBsThreads) void ms_block_sort_kernel(const uint32_
         const int diag = out0 - a0;
         const int i = ms_split([&](int x) { return sk[lp(a0 + x)]; }, [&](int x) { return sk[lp(b0 + x)]; }, L, L,
                                diag);
-        ms_merge16<HAS_VALUES, kBsTile>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
+        ms_merge16<HAS_VALUES, BTILE>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
     }
-    ms_store_tile<HAS_VALUES, kBsThreads>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
+    ms_store_tile<HAS_VALUES, BS>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -930,8 +929,16 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     if (n <= 0) return 0;
     if (mode < 0 || mode > 2 || (vin != nullptr) != (vout != nullptr) || (vin && !vtmp))
         return (int)hipErrorInvalidValue;
+    // block-sort tile (tuning knob merge_block: 8192 or 16384 keys; 0 = auto:
+    // 16384 for keys only from 4M keys -- one merge pass fewer for one more
+    // LDS round; measured 4M 0.194 -> 0.183 ms, 48M 1.52-1.55 -> 1.50, but
+    // 1M 0.099 -> 0.109 and key-value 48M 2.79 -> 2.90, where the 1024-lane
+    // blocks halve the resident blocks per CU; profiles/sort_r5.md)
+    const long mb = cme::tune_get(cme::kTuneMergeBlock);
+    const bool big = mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
+    const long long btile = big ? 2 * kBsTile : kBsTile;
     int npass = 0;
-    for (long long L = kBsTile; L < n; L <<= 1) ++npass;
+    for (long long L = btile; L < n; L <<= 1) ++npass;
     // the block sort writes where an even number of passes later lands in out
     uint32_t* d0 = (npass & 1) ? tmp : out;
     uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
@@ -943,17 +950,24 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     long part = ws ? cme::tune_get(cme::kTuneMergePart) : 0;
     if (part < 0) part = n >= (8ll << 20) ? 8 : 0;
     const int mtile = merge_tile(part != 0);
-    const unsigned btiles = cdiv(n, kBsTile), tiles = cdiv(n, mtile);
-    if (vin)
+    const unsigned btiles = cdiv(n, btile), tiles = cdiv(n, mtile);
+    const int m0 = npass ? 0 : mode;
+    if (big && vin)
+        hipLaunchKernelGGL((ms_block_sort_kernel<true, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s, in,
+                           d0, vin, v0, n, mode, m0);
+    else if (big)
+        hipLaunchKernelGGL((ms_block_sort_kernel<false, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s,
+                           in, d0, vin, v0, n, mode, m0);
+    else if (vin)
         hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode,
-                           npass ? 0 : mode);
+                           m0);
     else
         hipLaunchKernelGGL(ms_block_sort_kernel<false>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n,
-                           mode, npass ? 0 : mode);
+                           mode, m0);
     CME_TRY(hipGetLastError());
     const uint32_t *ki = d0, *vi = v0;
     int p = 0;
-    for (long long L = kBsTile; L < n; L <<= 1, ++p) {
+    for (long long L = btile; L < n; L <<= 1, ++p) {
         const bool last = p == npass - 1;
         uint32_t* ko = (ki == out) ? tmp : out;
         uint32_t* vo = vin ? ((vi == vout) ? vtmp : vout) : nullptr;

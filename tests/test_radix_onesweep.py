@@ -195,6 +195,28 @@ def test_merge_sort_partition_arms(gpu, part, tile):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block", [0, 8192, 16384])
+def test_merge_sort_block_tiles(gpu, block):
+    """Both block-sort tiles (tuning knob merge_block: 512 or 1024 lanes, or
+    the size rule)
+    sort keys and key-value pairs stably, with odd and even merge-pass counts
+    and partial last tiles."""
+    from cme213x.utils import tuning
+
+    g = torch.Generator(device="cuda").manual_seed(13)
+    with tuning.override(merge_block=block):
+        for n in (1, 100, 16383, 16385, 3 * 16384 + 7, 1 << 20, 9 * (1 << 20) + 3):
+            k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+            k[: n // 3] = k[: n // 3] % 5
+            v = torch.arange(n, device="cuda", dtype=torch.int32)
+            ks, vs = sort(k, values=v, algo="merge")
+            rk, ri = torch.sort(k.cpu().long(), stable=True)
+            assert torch.equal(ks.cpu().long(), rk), n
+            assert torch.equal(vs.cpu().long(), ri), n
+            assert torch.equal(sort(k, algo="merge").cpu().long(), rk), n
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("arm", [0, 1, 2, 3, 4, 5, 7, 8, 10, 14])
 def test_radix_downsweep_arms(gpu, arm):
     """Every reduce-then-scan downsweep arm (tuning knob radix_ds: atomic
