@@ -464,15 +464,15 @@ __device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
 // sequential merge of kMsItems outputs from A = [a0, a0+la) / B = [b0, b0+lb)
 // (logical LDS indices, padded on access) into registers. Branch-free: every
 // step selects its output, advances one of the two cursors and loads that
-// run's next key (the load address is always inside the buffer: CAP + 1
-// padded slots), so no lane diverges -- the divergent form spent more issue
+// run's next key (a cursor never passes its run's end, at most CAP: the
+// buffers hold CAP + 1 padded slots), so no lane diverges -- the divergent form spent more issue
 // slots on exec-mask bookkeeping than on the merge.
 template <bool HAS_VALUES, int CAP>
 __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* sv, int a0, int la, int b0, int lb,
                                            int i, int j, uint32_t (&k)[kMsItems], uint32_t (&v)[kMsItems]) {
-    int pa = a0 + i, pb = b0 + j;  // cursors (logical indices)
+    int pa = a0 + i, pb = b0 + j;  // cursors (logical indices; pa <= ea <= CAP, pb <= eb <= CAP)
     const int ea = a0 + la, eb = b0 + lb;
-    uint32_t ka = sk[lp(pa < ea ? pa : CAP)], kb = sk[lp(pb < eb ? pb : CAP)];
+    uint32_t ka = sk[lp(pa)], kb = sk[lp(pb)];
     ka = pa < ea ? ka : 0xffffffffu;
     kb = pb < eb ? kb : 0xffffffffu;
 #pragma unroll
@@ -485,9 +485,9 @@ __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* s
         }
         pa += take_a ? 1 : 0;
         pb += take_a ? 0 : 1;
-        const int np = take_a ? pa : pb;
+        const int np = take_a ? pa : pb;  // <= CAP: the spare slot at most
         const int ne = take_a ? ea : eb;
-        uint32_t nv = sk[lp(np < CAP ? np : CAP)];
+        uint32_t nv = sk[lp(np)];
         nv = np < ne ? nv : 0xffffffffu;
         ka = take_a ? nv : ka;
         kb = take_a ? kb : nv;
