@@ -480,12 +480,16 @@ int gated_pass(const T* p, T* c, int pitch, int gy, const int* r, int n, const i
 // runs; that is only safe if the two streams sit on different hardware
 // queues (with GPU_MAX_HW_QUEUES or a stream count that makes HIP share a
 // queue, the signal would wait behind the spinning kernel). One wave on the
-// compute stream spins (bounded: ~0.2 s) on a fresh device word that a
-// signal kernel on the comm stream sets; it reports 1 (seen) or 2 (gave up).
+// compute stream spins (bounded: ~2 s) on a fresh device word that a signal
+// kernel on the comm stream sets; it reports 1 (seen) or 2 (gave up). The
+// bound is generous because other processes sharing the GPU can delay the
+// signal kernel's dispatch for a time slice: a shorter bound (~0.2 s) gave a
+// false "shared queue" verdict once in the 8-processes-on-one-GPU test; a
+// true shared queue costs the full bound once, then the events schedule runs.
 __global__ __launch_bounds__(64) void gate_probe_kernel(const unsigned* flag, unsigned value, unsigned* result) {
     if (threadIdx.x != 0) return;
     unsigned r = 2u;
-    for (unsigned spins = 0; spins < (1u << 20); ++spins) {
+    for (unsigned spins = 0; spins < (1u << 23); ++spins) {
         const unsigned v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((int)(v - value) >= 0) {
             r = 1u;
