@@ -223,12 +223,12 @@ def main() -> int:
     ap.add_argument("--fma", type=int, choices=[0, 1], default=None,
                     help="1 = --arith fma, 0 = --arith exact")
     ap.add_argument("--arith", choices=["fma", "exact", "fast"], default=None,
-                    help="stencil arithmetic (default fma): fma = FMA-contracted (what nvcc emits for the "
-                         "reference's GPU kernel; <= 8 ULP of exact after 200 steps on random data), exact = no "
-                         "contraction (bitwise = the CPU oracle), fast = reassociated (CFL folded into the "
-                         "weights, symmetric pairs summed first: 17 instead of 20 flop-instructions per point; "
-                         "bitwise = the CPU fast oracle, but it drifts past the reference's 10-ULP criterion "
-                         "within 10 steps on random data: profiles/heat_arith_ulp_r5.md)")
+                    help="stencil arithmetic (default fast for the fp32 order-8 pipelined GPU pass, else fma): "
+                         "fma = FMA-contracted (what nvcc emits for the reference's GPU kernel; <= 8 ULP of exact "
+                         "after 200 steps on random data), exact = no contraction (bitwise = the CPU oracle), "
+                         "fast = reassociated (CFL folded into weights that sum to exactly one, symmetric pairs "
+                         "summed first: 17 instead of 20 flop-instructions per point; bitwise = the CPU fast "
+                         "oracle; <= 9 ULP of exact after whole runs: profiles/heat_arith_ulp_r5.md)")
     ap.add_argument("--tblock", type=int, choices=[0, 1, 2, 3, 4], default=0,
                     help="timesteps per halo exchange / per HBM pass (n > 1 = temporal blocking, nB-deep halos); "
                          "0 = by subdomain size (auto_tblock)")
@@ -261,7 +261,11 @@ def main() -> int:
     if args.share_gpu:
         args.transport = "ipc"
     if args.arith is None:
-        args.arith = "fma" if args.fma is None else ("fma" if args.fma else "exact")
+        if args.fma is None:
+            fast_ok = args.order == 8 and args.kernel == "pipe" and args.device == "cuda" and args.tblock in (0, 3, 4)
+            args.arith = "fast" if fast_ok else "fma"
+        else:
+            args.arith = "fma" if args.fma else "exact"
     args.fma = int(args.arith == "fma")
     # the solver's `fma` argument: False exact, True FMA-contracted, "fast" reassociated
     args.fma_arg = {"exact": False, "fma": True, "fast": "fast"}[args.arith]
@@ -515,8 +519,8 @@ def main() -> int:
                 "fma": bool(args.fma),
                 "arith": {"fma": "FMA-contracted (<= 10 ULP of exact: 8 at 4000^2 x 10, 7 at 2048^2 x 200 random)",
                           "exact": "exact (no contraction)",
-                          "fast": "reassociated (folded CFL weights, pair sums; drifts past 10 ULP of exact on "
-                                  "random data: 15 ULP at 4000^2 x 10 steps, 39 at 2048^2 x 200)"}[args.arith],
+                          "fast": "reassociated (folded CFL weights summing to exactly one, pair sums; <= 10 ULP "
+                                  "of exact: 9 at 4000^2 x 10 random, 7 at 2048^2 x 200 random)"}[args.arith],
                 "tblock": args.tblock,
                 "device": args.device,
                 "rehearsal_shared_gpu": bool(args.share_gpu),

@@ -215,14 +215,15 @@ def test_gpu_fast_pipe_gated_entry(gpu):
     assert torch.equal(out, ref) and int(tw.item()) == 0
 
 
-# measured max ULP distance from the exact stencil (interior cells) of the
-# reassociated arithmetic: it random-walks away from the exact trajectory and
-# leaves the reference's 10-ULP criterion within 10 steps on random data
-# (4000^2: 15 ULP, 5355 of 16M cells above 10; 2048^2 x 200 steps: 39 ULP,
-# 4.2M cells above 10), while the FMA-contracted stencil stays at <= 8
-# (profiles/heat_arith_ulp_r5.md). Hence FMA is the bench's default.
-_FAST_DRIFT_MAX = {(4000, 10, "uniform"): 10, (4000, 10, "random"): 16, (2048, 40, "random"): 13,
-                   (2048, 200, "random"): 40}
+# measured max ULP distance from the exact stencil (interior cells). The
+# reassociated arithmetic used to random-walk away from the exact trajectory
+# (15 ULP at 4000^2 x 10, 39 at 2048^2 x 200 random): its rounded fp32 weights
+# summed to 1 + ~1e-8. With weights that sum to exactly one
+# (heat_fast_make_consistent) it stays within the reference's 10-ULP criterion:
+# 7 / 9 / 7 / 7 ULP at the four shapes below, like the FMA form's <= 8
+# (profiles/heat_arith_ulp_r5.md).
+_FAST_DRIFT_MAX = {(4000, 10, "uniform"): 7, (4000, 10, "random"): 9, (2048, 40, "random"): 7,
+                   (2048, 200, "random"): 7}
 
 
 @pytest.mark.parametrize("arith", ["fma", "fast"])
@@ -235,9 +236,9 @@ def test_arith_ulp_drift_from_exact_at_scale(n, steps, flavor, init, arith):
     (4000^2, order 8, 10 steps: the reference's uniform IC and a random
     interior) and over 40- and 200-step 2048^2 runs on the bench's hw5 CFL
     numbers -- rounding differences compound with the step count. The
-    FMA-contracted arithmetic (what nvcc emits for the reference's GPU kernel;
-    the bench default) meets the criterion everywhere; the reassociated one
-    does not on random data, and its measured drift is pinned here. The GPU
+    FMA-contracted arithmetic (what nvcc emits for the reference's GPU kernel)
+    and the reassociated one with exactly-consistent weights (the bench
+    default) both meet it; the measured fast drift is pinned here. The GPU
     passes equal these CPU oracles bit for bit (test_gpu_fast_heat_run_bitwise,
     the pipe/stream FMA tests), so the numbers carry over to them."""
     from cme213x.utils.ulp import ulp_distance
@@ -260,5 +261,5 @@ def test_arith_ulp_drift_from_exact_at_scale(n, steps, flavor, init, arith):
     exact = heat_run(a, b, g.interior, 8, g.xcfl, g.ycfl, steps, "naive")
     xb, xe, yb, ye = g.interior
     d = int(ulp_distance(out[yb:ye, xb:xe].numpy(), exact[yb:ye, xb:xe].numpy()).max())
-    bound = 10 if arith == "fma" else _FAST_DRIFT_MAX[(n, steps, init)]
+    bound = 10 if arith == "fma" else min(10, _FAST_DRIFT_MAX[(n, steps, init)])
     assert d <= bound, f"{arith}: max {d} ULP"
