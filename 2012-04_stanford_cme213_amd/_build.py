@@ -72,29 +72,41 @@ def _cpu_flags() -> list[str]:
     ]
 
 
-def _newest_header() -> float:
-    return max((p.stat().st_mtime for p in INCLUDE.rglob("*.h")), default=0.0)
-
-
-def _local_includes(src: Path) -> list[Path]:
-    """Headers a source #includes by quoted relative path (heat_pipe.h is
-    shared by heat_pipe.hip and hip_tune/heat_pipe_tune.hip)."""
+def _includes(src: Path) -> list[Path]:
+    """Headers a source #includes by quoted path: "cme213/..." from csrc/
+    include, anything else relative to the source (heat_pipe.h is shared by
+    heat_pipe.hip and hip_tune/heat_pipe_tune.hip)."""
     out = []
     for line in src.read_text(errors="replace").splitlines():
         line = line.strip()
-        if line.startswith('#include "') and not line.startswith('#include "cme213/'):
-            h = (src.parent / line.split('"')[1]).resolve()
-            if h.exists():
-                out.append(h)
+        if not line.startswith('#include "'):
+            continue
+        name = line.split('"')[1]
+        h = (INCLUDE / name) if name.startswith("cme213/") else (src.parent / name)
+        h = h.resolve()
+        if h.exists():
+            out.append(h)
     return out
 
 
-def _needs(obj: Path, src: Path, hdr_time: float) -> bool:
-    if not obj.exists():
-        return True
-    t = obj.stat().st_mtime
-    local = max((h.stat().st_mtime for h in _local_includes(src)), default=0.0)
-    return src.stat().st_mtime > t or hdr_time > t or local > t
+def _dep_time(src: Path) -> float:
+    """Newest mtime over the source and every header it reaches (transitively),
+    so a header edit rebuilds only the objects that include it."""
+    seen: set[Path] = set()
+    stack = [src.resolve()]
+    newest = 0.0
+    while stack:
+        f = stack.pop()
+        if f in seen:
+            continue
+        seen.add(f)
+        newest = max(newest, f.stat().st_mtime)
+        stack.extend(_includes(f))
+    return newest
+
+
+def _needs(obj: Path, src: Path) -> bool:
+    return not obj.exists() or _dep_time(src) > obj.stat().st_mtime
 
 
 def _run(cmd: list[str]) -> None:
@@ -104,7 +116,6 @@ def _run(cmd: list[str]) -> None:
 
 
 def _compile_all(srcs: list[Path], kind: str, jobs: int, verbose: bool) -> list[Path]:
-    hdr = _newest_header()
     out_dir = OBJ_DIR / kind
     out_dir.mkdir(parents=True, exist_ok=True)
     tasks = []
@@ -112,7 +123,7 @@ def _compile_all(srcs: list[Path], kind: str, jobs: int, verbose: bool) -> list[
     for s in srcs:
         o = out_dir / (s.stem + ".o")
         objs.append(o)
-        if _needs(o, s, hdr):
+        if _needs(o, s):
             if kind in ("hip", "hip_tune"):
                 cmd = [HIPCC, *_hip_flags(), "-c", str(s), "-o", str(o)]
             else:

@@ -26,7 +26,7 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f32", "ppiipipiiffiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_f32", "ppiiiiiiiiffip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_f64", "ppiiiiiiiiddip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_f64", "ppiipipiiddiip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_streamn_tune", "ppiiiiiiffiiiip")
 _ext.proto(_ext.TUNE_PROTOS, "cme_heat_pipe_tune", "ppiiiiiiffiiiiip")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_run", "ippiiiddiiiiiipp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_dist_gate_status", "p")
@@ -37,13 +37,13 @@ _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f32", "ppiiiiiiiffp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_step_fast_f64", "ppiiiiiiiddp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_pipe_fast_f32", "ppiipipiiffiipupp")
 _ext.proto(_ext.HIP_PROTOS, "cme_heat_run_fast_f32", "ppiiiiiiiiffipp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_f32", "ppiiiiiiiiiffip")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_trace_f32", "ppiiiiiiiiiffippp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_status", "pi")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_flow_debug", "pi")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_f64", "ppiiiiiiiiiddippp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_f32", "ppiiiiiiiiiffippp")
-_ext.proto(_ext.HIP_PROTOS, "cme_heat_tile_res_status", "pi")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_flow_f32", "ppiiiiiiiiiffip")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_flow_trace_f32", "ppiiiiiiiiiffippp")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_flow_status", "pi")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_flow_debug", "pi")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_tile_res_f64", "ppiiiiiiiiiddippp")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_tile_res_f32", "ppiiiiiiiiiffippp")
+_ext.proto(_ext.TUNE_PROTOS, "cme_heat_tile_res_status", "pi")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f32", "ppiiiiiiff")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_step_f64", "ppiiiiiidd")
 _ext.proto(_ext.CPU_PROTOS, "cme_cpu_heat_run_f32", "ppiiiiiiffi")
@@ -277,7 +277,7 @@ def heat_run(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int]
 def heat_flow(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int, int], order: int, xcfl: float,
               ycfl: float, npass: int, fma="fma", ns: int = 4, trace: bool = False):
     """``npass`` four-step passes of the whole ``region`` as ONE persistent
-    dataflow launch (csrc/hip/heat_flow.hip: tasks pulled from a ticket, each
+    dataflow launch (csrc/hip_tune/heat_flow.hip, tuning library: tasks pulled from a ticket, each
     waiting for the 3 x 3 neighbourhood of the previous pass). fp32, order 8,
     GPU; ``fma``: "exact" / False, "fma" / True, or "fast". Bit for bit the
     result of ``npass`` one-pass launches (``heat_run`` with the knob
@@ -326,7 +326,7 @@ def heat_tile_res(a: torch.Tensor, b: torch.Tensor, region: tuple[int, int, int,
                   ycfl: float, npass: int, ns: int = 2, fma: bool = False, trace: bool = False):
     """``npass`` passes of ``ns`` (2, or 4 at order 8) steps of the whole
     ``region`` with every 64 x 64 tile resident in LDS for the whole run, in
-    ONE cooperative launch (csrc/hip/heat_tile_res.hip: only the NS*B-deep
+    ONE cooperative launch (csrc/hip_tune/heat_tile_res.hip, tuning library: only the NS*B-deep
     halo ring moves, behind the tile's inner cone). GPU, fp32 / fp64, orders
     2 / 4 / 8; bit for bit the result of single steps of the same arithmetic.
     Returns the buffer holding the result (``b`` for odd ``npass``), or with

@@ -18,7 +18,7 @@ def main():
     from cme213x.ops.elementwise import copy_
     from cme213x.utils.params import SimParams
 
-    _ext.proto(_ext.HIP_PROTOS, "cme_heat_stream_tune_f32", "ppiiiiiiffiiiip")
+    _ext.proto(_ext.TUNE_PROTOS, "cme_heat_stream_tune_f32", "ppiiiiiiffiiiip")
     n = int(os.environ.get("TUNE_N", "16384"))
     p = SimParams(nx=n, ny=n, order=8)
     g = HeatGrid(p, torch.float32, "cuda")

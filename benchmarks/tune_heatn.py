@@ -22,7 +22,7 @@ def main():
     from cme213x.models.heat2d import HeatGrid
     from cme213x.utils.params import SimParams
 
-    _ext.proto(_ext.HIP_PROTOS, "cme_heat_stream2_tune", "ppiiiiiiiddiiiip")
+    _ext.proto(_ext.TUNE_PROTOS, "cme_heat_stream2_tune", "ppiiiiiiiddiiiip")
     n = int(os.environ.get("TUNE_N", "16384"))
     s = _ext.stream_ptr()
     p = SimParams(nx=n, ny=n, order=8)

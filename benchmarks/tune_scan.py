@@ -15,7 +15,7 @@ def main():
     from cme213x import _ext
     from cme213x.ops.scan import workspace
 
-    _ext.proto(_ext.HIP_PROTOS, "cme_scan_tune", "ppqiipp")
+    _ext.proto(_ext.TUNE_PROTOS, "cme_scan_tune", "ppqiipp")
     n = 1 << 26
     x = torch.rand(n, device="cuda")
     y = torch.empty_like(x)
@@ -72,7 +72,7 @@ def spmv_main():
     from cme213x.models.spmv_scan import BENCH_SHAPES, SpmvScanSolver, generate
     from cme213x.ops.scan import _run_ws
 
-    _ext.proto(_ext.HIP_PROTOS, "cme_spmv_scan_tune", "pppqipiip")
+    _ext.proto(_ext.TUNE_PROTOS, "cme_spmv_scan_tune", "pppqipiip")
     s = _ext.stream_ptr()
     mats = os.environ.get("CME_SPMV_MATS", "pwtk webbase-1M mac_econ_fwd500 jonheart").split()
     modes = [int(m) for m in os.environ.get("CME_SPMV_MODES", "0 1 2 3 6 7").split()]

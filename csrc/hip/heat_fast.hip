@@ -118,9 +118,6 @@ CME_EXPORT int cme_heat_pipe_fast_f32(const float* prev, float* curr, int pitch,
     }
 }
 
-extern "C" int cme_heat_flow_f32(float* a, float* b, int pitch, int gy, int xb, int xe, int yb, int ye, int order,
-                                 int arith, int ns, float xcfl, float ycfl, int npass, void* stream);
-
 // iters reassociated timesteps of the whole region [xb, xe) x [yb, ye) from
 // `a` (every cell outside it holds the same fixed value in a and b): passes
 // of ns (1-4) steps, the remainder as one shorter pass (a single step on the
@@ -132,14 +129,6 @@ CME_EXPORT int cme_heat_run_fast_f32(float* a, float* b, int pitch, int gy, int 
     float* bufs[2] = {a, b};
     int cur = 0;
     int i = 0;
-    if (ns == 4 && iters >= 2 * ns && cme::tune_get(cme::kTuneHeatFlow) != 0) {
-        // all whole passes as ONE persistent dataflow launch (heat_flow.hip)
-        const int np = iters / ns;
-        const int rc = cme_heat_flow_f32(a, b, pitch, gy, xb, xe, yb, ye, order, 2, ns, xcfl, ycfl, np, stream);
-        if (rc) return rc;
-        cur = np & 1;
-        i = np * ns;
-    }
     while (i < iters) {
         const int k = iters - i < ns ? iters - i : ns;
         const int rc = k >= 2 ? cme_heat_pipe_fast_f32(bufs[cur], bufs[cur ^ 1], pitch, gy, r, 1, r, order, k, xcfl,

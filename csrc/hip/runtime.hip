@@ -93,9 +93,9 @@ const TuneEntry kTuneTable[cme::kTuneCount] = {
     {"CME_STREAMN_CHUNK", 0},    {"CME_STREAMN_ROUNDS", 0},     {"CME_STREAMN_MINCHUNK", 0},
     {"CME_STREAMN_THIN_WAVES", 1024}, {"CME_STREAMN_CAPPCT", 100}, {"CME_SPMVSCAN_MULTI", 1},
     {"CME_SPMV_NT", 2},          {"CME_SPMV_DIA1", 0},          {"CME_PIPE_TAPER", 0},
-    {"CME_RADIX_UP_UNR", 4},     {"CME_RADIX_OS_LANES", 1},     {"CME_HEAT_FLOW", 0},
+    {"CME_RADIX_UP_UNR", 4},     {"CME_RADIX_OS_LANES", 1},
     {"CME_FLOW_PER_CU", 0},      {"CME_FLOW_SPINS", 1L << 22},  {"CME_FLOW_MODE", 0},
-    {"CME_SPMV_STREAM_ROWS", 0}, {"CME_TILE_RES", 0},           {"CME_TILE_RES_NS", 2},
+    {"CME_SPMV_STREAM_ROWS", 0},
     {"CME_TILE_RES_MINR", 1},    {"CME_SPMV_SHORT_RPT", 1},     {"CME_MERGE_PART", -1},
     {"CME_MERGE_TILE", 4096},    {"CME_MERGE_BLOCK", 0},
 };

@@ -48,7 +48,7 @@
 // an explicit s_waitcnt lgkmcnt(0) before the barrier the other waves read it
 // behind; the compiler emitted none, and waves then ran the previous ticket
 // (two tasks wrong in ~1 run of 5 at 4096^2).
-#include "heat_pipe.h"
+#include "../hip/heat_pipe.h"
 #include "cme213/persist_ws.h"
 
 using namespace cme;
@@ -219,9 +219,36 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
 
 // per-call control words + completion words + give-up records
 // (cme213/persist_ws.h), zeroed by one memset node
-PersistWs& flow_ws() {
-    static PersistWs w;
-    return w;
+PersistWs& flow_ws() { return persist_ws_for<0>(); }
+
+// The XCD bands assume workgroups on all 8 XCDs with XCC_ID 0..7 (the full
+// MI355X in SPX mode): band x is served only by XCD x's workgroups. A probe
+// launch records the XCC_IDs the dispatcher actually uses (vector atomics);
+// any other set -- a CPX / DPX compute partition, a part with fewer XCDs --
+// makes the launcher take the single-queue schedule (OST = 0), which needs
+// no band. Cached per device.
+__global__ void xcc_probe_kernel(unsigned* mask) {
+    if (threadIdx.x == 0) atomicOr(mask, 1u << (__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 31));  // HW_REG_XCC_ID
+}
+
+int xcd_bands_ok(bool* ok) {
+    static int cached[64];  // 0 unknown, 1 all 8 bands served, 2 not
+    int dev = 0;
+    CME_TRY(hipGetDevice(&dev));
+    int& c = cached[dev & 63];
+    if (c == 0) {
+        unsigned* m = nullptr;
+        CME_TRY(hipMalloc(&m, 4));
+        CME_TRY(hipMemset(m, 0, 4));
+        hipLaunchKernelGGL(xcc_probe_kernel, dim3(64 * device_cu_count()), dim3(64), 0, nullptr, m);
+        CME_TRY(hipGetLastError());
+        unsigned h = 0;
+        CME_TRY(hipMemcpy(&h, m, 4, hipMemcpyDeviceToHost));
+        CME_TRY(hipFree(m));
+        c = h == 0xffu ? 1 : 2;
+    }
+    *ok = c == 1;
+    return 0;
 }
 
 constexpr size_t kCtlWords = kCtlStride * (kBands + 1);
@@ -304,7 +331,14 @@ int launch_flow(T* a, T* b, int pitch, int gy, Region g, T xcfl, T ycfl, int npa
 template <int FMA>
 int flow_arith(float* a, float* b, int pitch, int gy, Region g, float xcfl, float ycfl, int npass, hipStream_t s,
                unsigned long long* trace, int* ntasks) {
-    if (cme::tune_get(cme::kTuneFlowMode) & 4096)  // diagnostics: one queue, a release fence per task
+    bool bands = false;
+    {
+        const int rc = xcd_bands_ok(&bands);
+        if (rc) return rc;
+    }
+    // diagnostics (mode 4096), or not the 8 XCC_IDs the bands need: one
+    // queue, a release fence per task
+    if (!bands || (cme::tune_get(cme::kTuneFlowMode) & 4096))
         return launch_flow<float, 8, 4, FMA, 2, 1, true, 1, 8, 3, 0>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace,
                                                                     ntasks);
     return launch_flow<float, 8, 4, FMA, 2, 1, true, 1, 8, 3, 2>(a, b, pitch, gy, g, xcfl, ycfl, npass, s, trace,

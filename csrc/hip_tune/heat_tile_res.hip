@@ -45,7 +45,7 @@
 // workgroup leaves at its next wait -- and the sticky pinned timeout word of
 // cme_heat_tile_res_status. The launch is cooperative, so a grid that cannot
 // be co-resident is refused at launch instead of deadlocking.
-#include "heat_tile.h"
+#include "../hip/heat_tile.h"
 #include "cme213/persist_ws.h"
 #include "cme213/tuning.h"
 
@@ -302,9 +302,8 @@ __global__ __launch_bounds__(NT) void heat_tile_res_kernel(T* a, T* b, int pitch
     }
 }
 
-PersistWs& res_ws() {  // abort word + completion words (cme213/persist_ws.h)
-    static PersistWs w;
-    return w;
+PersistWs& res_ws() {  // abort word + completion words (cme213/persist_ws.h), per device
+    return persist_ws_for<1>();
 }
 
 constexpr int kCtlWords = 64;

@@ -2,8 +2,9 @@
 // (heat_flow.hip, heat_tile_res.hip): device words zeroed by one memset per
 // call (tickets, completion words, abort word, give-up records) and a pinned
 // host word the kernels set when a wait gives up -- sticky, read after the
-// stream is synchronised. One block per launch family: the family's launches
-// are serialised on their stream.
+// stream is synchronised. One block per launch family and device
+// (persist_ws_for): the family's launches on a device are serialised on
+// their stream, and a device switch never reuses another device's memory.
 #pragma once
 
 #include "cme213/common.h"
@@ -39,5 +40,14 @@ struct PersistWs {
         return v;
     }
 };
+
+// The control block of launch family F on the current device (up to 64).
+template <int F>
+PersistWs& persist_ws_for() {
+    static PersistWs blocks[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return blocks[dev & 63];
+}
 
 }  // namespace cme

@@ -35,13 +35,10 @@ enum TuneKey : int {
     kTunePipeTaper,        // CME_PIPE_TAPER: half-height last chunks per strip of a multi-round pass (0 off, -1 auto)
     kTuneRadixUpUnr,       // CME_RADIX_UP_UNR: radix upsweep 16-B loads in flight per lane (4, 8, 16)
     kTuneRadixOsLanes,     // CME_RADIX_OS_LANES: onesweep ranks, 1 lane order where the probe passed, 0 ballot match
-    kTuneHeatFlow,         // CME_HEAT_FLOW: 1 multi-pass heat runs as one persistent dataflow launch (heat_flow.hip), 0 (default) a launch per pass
     kTuneFlowPerCU,        // CME_FLOW_PER_CU: task target per CU of the dataflow launch (0 = the pipelined pass's rule)
     kTuneFlowSpins,        // CME_FLOW_SPINS: polls of a dataflow dependency wait before it gives up
     kTuneFlowMode,         // CME_FLOW_MODE: diagnostics of the dataflow hand-off (fence scopes)
     kTuneSpmvStreamRows,   // CME_SPMV_STREAM_ROWS: CSR-stream rows per block (0 = by mean row length)
-    kTuneTileRes,          // CME_TILE_RES: 1 tileN heat runs keep the tiles resident in LDS across passes (heat_tile_res.hip; default 0: measured slower)
-    kTuneTileResNs,        // CME_TILE_RES_NS: steps per halo exchange of the resident tiles (2 or 4)
     kTuneTileResMinR,      // CME_TILE_RES_MINR: rows per band at least in the resident tiles' steps
     kTuneSpmvShortRpt,     // CME_SPMV_SHORT_RPT: CSR-short rows per lane (1, 2, 4)
     kTuneMergePart,        // CME_MERGE_PART: merge sort partitions: 4 / 8 / 16 / 32 / 64 lanes per tile in one search launch per pass (other positive: 64), 0 in-block searches, -1 auto (8 from 8M keys)

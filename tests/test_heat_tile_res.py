@@ -1,11 +1,13 @@
-"""Resident LDS tiles across a whole run (csrc/hip/heat_tile_res.hip): one
+"""Resident LDS tiles across a whole run (csrc/hip_tune/heat_tile_res.hip,
+tuning library only: measured slower than per-pass tile launches,
+profiles/heat_tile_res_r5.md; the GPU tests skip without it): one
 cooperative launch keeps every 64 x 64 tile in LDS, exchanges only the
 NS*B-deep halo ring with its 8 neighbours per pass, and hides the exchange
 behind the tile's inner cone.
 
 Parity: bit for bit the CPU oracle's single steps of the same arithmetic
 (the reference's 10-ULP check, hw/hw5/2dHeat_solution.cpp, met with zero
-ULP), and the per-pass tile launches (knob tile_res = 0). Shapes: the hw5
+ULP), and the per-pass tile launches (production heat_run). Shapes: the hw5
 1000^2, grids that are not multiples of the tile (ragged right / bottom
 tiles, tiles narrower than the halo), a single tile; orders 2 / 4 / 8,
 fp32 / fp64, exact / FMA, 2 and 4 steps per exchange."""
@@ -42,7 +44,7 @@ def _cpu_steps(g, n, fma):
 @pytest.mark.parametrize("fma", [False, True])
 @pytest.mark.parametrize("shape,npass", [((1000, 1000), 3), ((333, 190), 5), ((130, 77), 2), ((64, 64), 4),
                                          ((70, 600), 1)])
-def test_resident_equals_cpu_oracle(gpu, dtype, order, ns, fma, shape, npass):
+def test_resident_equals_cpu_oracle(gpu, tune_lib, dtype, order, ns, fma, shape, npass):
     g = _grid(*shape, order, dtype, gpu, seed=npass)
     want = _cpu_steps(g, ns * npass, fma)
     a, b = g.buf[0].clone(), g.buf[1].clone()
@@ -54,23 +56,23 @@ def test_resident_equals_cpu_oracle(gpu, dtype, order, ns, fma, shape, npass):
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,fma", [("tile4", False), ("tile4_fma", True), ("tile2", False)])
 @pytest.mark.parametrize("iters,res_ns", [(13, 2), (13, 4), (100, 2)])
-def test_heat_run_resident_equals_tile_passes(gpu, variant, fma, iters, res_ns):
-    """heat_run's tile variants run the resident launch (whole exchanges) plus
-    a tile-pass tail; bitwise the per-pass tile launches (knob off)."""
-    from cme213x.utils import tuning
-
+def test_resident_plus_tail_equals_tile_passes(gpu, tune_lib, variant, fma, iters, res_ns):
+    """The resident launch over whole exchanges plus a tile-pass tail is
+    bitwise the per-pass tile launches of production heat_run."""
     g = _grid(1000, 1000, 8, torch.float64, gpu, seed=iters)
-    with tuning.override(tile_res=0):
-        ref = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, variant).clone()
-    with tuning.override(tile_res=1, tile_res_ns=res_ns):
-        out = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, variant)
+    ref = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, iters, variant).clone()
+    np_ = iters // res_ns
+    a, b = g.buf[0].clone(), g.buf[1].clone()
+    mid = heat_tile_res(a, b, g.interior, 8, g.xcfl, g.ycfl, np_, ns=res_ns, fma=fma)
+    other = a if mid.data_ptr() == b.data_ptr() else b
+    out = heat_run(mid, other, g.interior, 8, g.xcfl, g.ycfl, iters - np_ * res_ns, variant)
     torch.cuda.synchronize()
     assert not tile_res_timed_out(reset=True)
     assert torch.equal(out, ref)
 
 
 @pytest.mark.gpu
-def test_resident_trace_and_schedule(gpu):
+def test_resident_trace_and_schedule(gpu, tune_lib):
     """Every (pass, tile) is stamped in order (start <= inner done <= halo in
     <= outer done <= ring published, the last during the next pass), and a
     tile's halo of pass p + 1 is read only after each of its 8 neighbours
@@ -95,23 +97,15 @@ def test_resident_trace_and_schedule(gpu):
 
 
 @pytest.mark.gpu
-def test_resident_too_large_falls_back(gpu):
-    """More tiles than the device holds at once: the direct call refuses,
-    heat_run falls back to tile passes (same bits)."""
-    from cme213x.utils import tuning
-
+def test_resident_too_large_falls_back(gpu, tune_lib):
+    """More tiles than the device holds at once: the call refuses."""
     g = _grid(2200, 2000, 8, torch.float64, gpu, seed=2)  # 35 x 32 tiles > one per CU
     with pytest.raises(ValueError, match="resident"):
         heat_tile_res(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 2)
-    with tuning.override(tile_res=0):
-        ref = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 6, "tile4").clone()
-    with tuning.override(tile_res=1):
-        out = heat_run(g.buf[0].clone(), g.buf[1].clone(), g.interior, 8, g.xcfl, g.ycfl, 6, "tile4")
-    assert torch.equal(out, ref)
 
 
 @pytest.mark.gpu
-def test_resident_timeout_raises_and_drains(gpu):
+def test_resident_timeout_raises_and_drains(gpu, tune_lib):
     """A neighbour wait that gives up (diagnostics: tile 0 never publishes)
     aborts every workgroup and raises; the next call runs."""
     from cme213x.utils import tuning
