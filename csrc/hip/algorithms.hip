@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kThreads) void select_lookback_kernel(const U* __re
             const int pre = lb2_lookback<int>(lbv, tile, ntiles, tile_sel, 0u, timeout);
             if (lane == 0) s_pre = pre;
         }
-        __syncthreads();
+        lds_bcast_sync();
         const long long sel_off = s_pre;
         for (int k = threadIdx.x; k < tile_sel; k += kThreads) o[sel_off + k] = stage[k];
         if (tile == ntiles - 1 && threadIdx.x == 0) *count_out = sel_off + tile_sel;

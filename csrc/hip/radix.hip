@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kOsThreads, HAS_VALUES ? 2 : 4) void radix_onesweep
             }
             if (lane == 0) s_K = K;
         }
-        __syncthreads();
+        lds_bcast_sync();
         const int K = s_K;
         {
             const int d = tid & (kBins - 1), h = tid >> 8;

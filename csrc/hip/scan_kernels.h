@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
         }
     }
     if (lane == 0) s_wtot[parity][wid] = run;
-    __syncthreads();
+    lds_bcast_sync();
     T wpre = T(0), tot = T(0);
 #pragma unroll
     for (int w = 0; w < kScanWaves; ++w) {
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const T* __
             for (int k = 0; k < ROWS; ++k) vn[k] = load_v4(in, nb + k * 256 + lane * 4, n, T(0));
         }
     }
-    __syncthreads();
+    lds_bcast_sync();
     const T p = s_prefix[parity] + wpre;
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void rts_scan_kernel(const T* __restrict__ in,
             }
         }
         if (lane == 0) s_wtot[parity][wid] = run;
-        __syncthreads();
+        lds_bcast_sync();
         T wpre = T(0), tot = T(0);
 #pragma unroll
         for (int w = 0; w < kScanWaves; ++w) {
@@ -439,21 +439,21 @@ __device__ __forceinline__ T tree_block_exclusive(T v, T* s, T* s2, T& total) {
         int offset = 1;
 #pragma unroll
         for (int d = kWave / 2; d > 0; d >>= 1) {  // up-sweep (reduce)
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             if (lane < d) {
                 const int ai = offset * (2 * lane + 1) - 1, bi = offset * (2 * lane + 2) - 1;
                 sw[cf(bi)] += sw[cf(ai)];
             }
             offset <<= 1;
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const T wtot = sw[cf(kWave - 1)];
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         if (lane == 0) sw[cf(kWave - 1)] = T(0);
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {  // down-sweep
             offset >>= 1;
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             if (lane < d) {
                 const int ai = offset * (2 * lane + 1) - 1, bi = offset * (2 * lane + 2) - 1;
                 const T x = sw[cf(ai)];
@@ -461,7 +461,7 @@ __device__ __forceinline__ T tree_block_exclusive(T v, T* s, T* s2, T& total) {
                 sw[cf(bi)] += x;
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         T r = sw[cf(lane)];
         // the wave totals (stored past the 4 segments), one barrier
         T* st = s + 4 * (kWave + kWave / 32);
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(kScanThreads) void segscan_kernel(const float* __re
             }
         }
     }
-    __syncthreads();
+    lds_bcast_sync();
     // carry into this wave: tile prefix unless a head precedes in the tile
     const float tile_pre = s_prefix;
     const float wcarry = wpre_f ? wpre_v : tile_pre + wpre_v;

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(DS_THREADS, DS_THREADS == 512 ? 2 : 1) void radix_d
         const uint32_t db = block_exclusive_scan<kWavesD>(td, s_t, tot, OpAdd());
         if (tid < kBins) s_base[tid] = db + prefix[(size_t)tid * nblocks + blockIdx.x];
         if (tid < kBins && td == (uint32_t)n) s_identity = 1;  // every key has this digit
-        __syncthreads();
+        lds_bcast_sync();
     }
     if (s_identity) {
         // one digit holds every key: the stable pass is the identity
@@ -765,10 +765,10 @@ __global__ __launch_bounds__(256) void radix_lane_order_probe_kernel(int trials,
             const int onl = __shfl((int)on, l);
             lower += (l < lane && onl && dl == d) ? 1u : 0u;
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         uint32_t old = 0;
         if (on) old = atomicAdd(&cnt[w][d], 1u);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         nbad += (on && old != before + lower) ? 1u : 0u;
     }
     if (nbad) atomicAdd(bad, nbad);

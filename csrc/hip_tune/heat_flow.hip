@@ -46,10 +46,13 @@
 //
 // LDS hazard found on the way: lane 0's LDS write of the next ticket needs
 // an explicit s_waitcnt lgkmcnt(0) before the barrier the other waves read it
-// behind; the compiler emitted none, and waves then ran the previous ticket
-// (two tasks wrong in ~1 run of 5 at 4096^2).
+// behind -- hipcc drops the one __syncthreads() carries when the barrier heads
+// the loop and the write ends the body (profiles/lds_broadcast_isa_r6.md) --
+// and waves then ran the previous ticket (two tasks wrong in ~1 run of 5 at
+// 4096^2). cme::lds_bcast_sync (wave.h) is the wait + barrier.
 #include "../hip/heat_pipe.h"
 #include "cme213/persist_ws.h"
+#include "cme213/wave.h"
 
 using namespace cme;
 
@@ -114,14 +117,11 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
         if (__hip_atomic_load(f.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) tk = total;
         s_ticket = tk;
         s_stop = 0;
-        // the LDS write must be complete before this wave reaches the barrier
-        // the other waves read it behind (see the header)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (f.trace) t_tk = wall_clock64();
     };
     if (threadIdx.x == 0) fetch();
     for (;;) {
-        __syncthreads();
+        lds_bcast_sync();  // lane 0's ticket write (wave.h: the loop-head barrier case)
         const int t = __builtin_amdgcn_readfirstlane(s_ticket);
         if (t >= total) break;
         const int pass = t / btasks, local = t - pass * btasks;
@@ -179,9 +179,8 @@ __global__ __launch_bounds__(NS * WPR * 64, (OCC > 0 ? 4 * OCC / NS : 1)) void h
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (give_up && lane == 0) s_stop = 1;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
-            __syncthreads();
+            lds_bcast_sync();
             if (__builtin_amdgcn_readfirstlane(s_stop)) break;
         }
         unsigned long long t_start = 0;

@@ -13,6 +13,34 @@
 
 namespace cme {
 
+// LDS hand-offs between lanes / waves -- the two documented patterns
+// (ISA-verified: scripts/check_lds_barriers.py, profiles/lds_broadcast_isa_r6.md).
+//
+// lds_bcast_sync(): a value one lane (or a few) wrote to LDS, read by the
+// other waves of the workgroup. The writers' ds_write must have completed
+// before the barrier lets the readers go: __syncthreads() normally carries an
+// s_waitcnt lgkmcnt(0) for that, but hipcc drops it when the barrier heads a
+// loop and the write sits at the end of the loop body (the dataflow launch's
+// ticket loop), so the wait is explicit here. Every wave executes it (it only
+// waits for the wave's own LDS operations; free where the compiler already
+// waits).
+__device__ __forceinline__ void lds_bcast_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// wave_lds_sync(): LDS written by some lanes of a wave and read by other
+// lanes of the SAME wave (in-wave trees). A wave's LDS operations execute in
+// order, so no s_waitcnt is needed; __builtin_amdgcn_wave_barrier is only a
+// convergence / scheduling barrier that does not order memory, so the
+// wavefront-scope fences keep the optimiser from moving or forwarding LDS
+// accesses across it (they emit no instruction).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // DPP control codes (GFX9 encoding; gfx950 is GFX9-family).
 enum : int {
     kDppRowShr1 = 0x111,
@@ -131,7 +159,7 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* lds, T& total, Op op =
     T wtot;
     T ex = wave_exclusive_scan<Op>(v, &wtot, op);
     if (lane == 0) lds[wid] = wtot;
-    __syncthreads();
+    lds_bcast_sync();
     T carry = Op::template identity<T>();
     T run = Op::template identity<T>();
 #pragma unroll
@@ -151,7 +179,7 @@ __device__ __forceinline__ T block_reduce(T v, T* lds, Op op = Op()) {
     const int wid = threadIdx.x / kWave;
     T w = wave_reduce<Op>(v, op);
     if (lane == 0) lds[wid] = w;
-    __syncthreads();
+    lds_bcast_sync();
     T run = Op::template identity<T>();
 #pragma unroll
     for (int i = 0; i < NW; ++i) run = op(run, lds[i]);
