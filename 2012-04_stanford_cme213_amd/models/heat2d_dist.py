@@ -722,19 +722,29 @@ class DistHeat:
     # -- native loop selection (run) ------------------------------------
     def enable_native(self, transport: str | None = None, fused: bool = True) -> dict:
         """One-time, collective setup of the native loop that :meth:`run`
-        uses on the GPU (``native="auto"`` / ``"on"``). Picks the transport
-        -- loopback when every subdomain is in this process, RCCL over an
-        ``nccl`` group, IPC-mapped peers over a ``gloo`` group on the GPU (the
-        shared-GPU rehearsal) or as ``transport`` says -- then checks the
-        native loop bit for bit against the Python loop on a small problem of
-        the same decomposition (:func:`native_selftest`): first with the
-        fused one-launch schedule, then (if that fails) schedule 0. Every
-        rank agrees on each step, so no rank is left alone in a collective.
-        With ``"auto"`` a failure leaves :meth:`run` on the Python loop;
-        with ``"on"`` it raises. Returns :attr:`native_info`."""
+        uses on the GPU (``native="auto"`` / ``"on"``). Transports are tried
+        in order until one passes (:func:`choose_native_transport`):
+
+        * every subdomain in this process: loopback;
+        * an ``nccl`` group: RCCL, then IPC-mapped peers (the neighbours'
+          grids mapped with hipIpcOpenMemHandle and pulled over xGMI);
+        * a ``gloo`` group on the GPU (the shared-GPU rehearsal): IPC;
+        * ``transport``: one kind ("rccl", "ipc") or a comma-separated chain
+          ("rccl,ipc").
+
+        Each candidate is opened and then checked bit for bit against the
+        Python loop on a small problem of the same decomposition
+        (:func:`native_selftest`): with the fused one-launch schedule, then
+        schedule 0. Every rank agrees on every step, so all ranks move to the
+        next candidate together and none is left alone in a collective. If
+        none passes, ``"auto"`` leaves :meth:`run` on the torch.distributed
+        loop and ``"on"`` raises. Returns :attr:`native_info`, with the
+        chain's record under ``"attempts"`` (hw/hw5/2dHeat_solution.cpp:
+        630-664 is the reference's one, MPI-only, multi-process run)."""
         if self.native_info is not None:
             return self.native_info
-        info = {"loop": "python", "transport": None, "fused_allowed": False, "selftest": None, "schedule": None}
+        info = {"loop": "python", "transport": None, "fused_allowed": False, "selftest": None, "schedule": None,
+                "attempts": []}
         self.native_info = info
         if self.native_mode == "off" or self.device.type != "cuda" or self.solo():
             return info
@@ -745,44 +755,46 @@ class DistHeat:
             self.comm.allreduce_(t, "min")
             return bool(t.item() == 1.0)
 
-        kind = "loopback"
         # RCCL may be asked for at world 1 too (a periodic grid's halos are
         # then self-sends); IPC needs other processes to map
-        need_transport = self.comm.size > 1 or transport == "rccl"
-        if need_transport:
+        if self.comm.size > 1 or transport is not None:
             backend = getattr(self.comm, "backend", None)
-            kind = transport or ("rccl" if backend == "nccl" else "ipc")
+            kinds = (transport.split(",") if transport else (["rccl", "ipc"] if backend == "nccl" else ["ipc"]))
+        else:
+            kinds = ["loopback"]
+        group = getattr(self.comm, "group", None)
 
-        def open_transport():
+        def open_transport(kind):
+            if kind == "loopback":
+                return None
             if kind == "rccl":
                 from ..parallel.rccl import NativeRccl
 
-                return NativeRccl(getattr(self.comm, "group", None))
-            from ..parallel.ipc import NativeIpc
+                return NativeRccl(group)
+            if kind == "ipc":
+                from ..parallel.ipc import NativeIpc
 
-            return NativeIpc(getattr(self.comm, "group", None))
+                return NativeIpc(group)
+            raise ValueError(f"unknown native transport {kind!r}")
 
-        ok, handle = native_setup_agreement(agree, _ext.hip, open_transport if need_transport else None,
-                                            f"DistHeat rank {self.comm.rank}", kind)
-        if ok:
-            ok = False
-            for f in ((True, False) if fused else (False,)):
-                try:
-                    good = native_selftest(self, kind, handle, f)
-                except Exception as e:  # noqa: BLE001 - e.g. the gated grid refused, a timed-out wait
-                    print(f"DistHeat rank {self.comm.rank}: native self-test raised ({e})", flush=True)
-                    good = False
-                if agree(good):
-                    ok, fused = True, f
-                    break
-        if not ok:
-            if handle is not None and kind == "rccl":
+        def release(kind, handle):
+            if handle is None:
+                return
+            if kind == "rccl":
                 handle.abort()  # pending native sends/recvs fail on the peers instead of hanging
+            elif kind == "ipc":
+                handle.close()  # collective: every rank reached the self-test with a handle
+
+        kind, handle, fused_ok, attempts = choose_native_transport(
+            kinds, agree, _ext.hip, open_transport, lambda k, h, f: native_selftest(self, k, h, f), release,
+            (True, False) if fused else (False,), f"DistHeat rank {self.comm.rank}")
+        info["attempts"] = attempts
+        if kind is None:
             if self.native_mode == "on":
-                raise RuntimeError("native distributed loop failed its setup or bitwise self-test")
+                raise RuntimeError(f"native distributed loop failed its setup or bitwise self-test ({attempts})")
             return info
         self._native = (kind, handle)
-        info.update(loop="native", transport=kind, fused_allowed=fused, selftest=True)
+        info.update(loop="native", transport=kind, fused_allowed=fused_ok, selftest=True)
         return info
 
     def _run_native_selected(self, iters: int, sync: bool | None) -> None:
@@ -979,6 +991,46 @@ def native_setup_agreement(agree, load_lib, open_transport, who: str = "", kind:
             ok = False
         ok = agree(ok)
     return ok, handle
+
+
+def choose_native_transport(kinds, agree, load_lib, open_transport, selftest, release, schedules=(True, False),
+                            who: str = "") -> tuple:
+    """The transport chain of :meth:`DistHeat.enable_native` (collective).
+    Loads the native library once, then for each kind in ``kinds``: opens it
+    (``open_transport(kind)``) and runs ``selftest(kind, handle, fused)``
+    for each schedule in ``schedules`` (fused first) until one passes --
+    every step followed by ``agree`` (an all-rank AND), so every rank makes
+    the same calls and moves to the next kind together. A kind whose
+    self-test failed on any rank is released (``release(kind, handle)``:
+    RCCL abort, IPC unmap) before the next is opened. Returns ``(kind,
+    handle, fused, attempts)`` -- ``kind`` None if no candidate passed --
+    with ``attempts`` = [{"transport", "result"[, "fused"]}] in the order
+    tried (result "ok", "library", "setup" or "selftest")."""
+    attempts = []
+    ok, _ = native_setup_agreement(agree, load_lib, None, who)
+    if not ok:
+        return None, None, False, [{"transport": kinds[0] if kinds else None, "result": "library"}]
+    for kind in kinds:
+        ok, handle = native_setup_agreement(agree, lambda: None, lambda k=kind: open_transport(k), who, kind)
+        if not ok:
+            # a communicator this rank opened while a peer failed: RCCL's
+            # abort is local; an IPC handle holds no mapping yet
+            if handle is not None and kind == "rccl":
+                release(kind, handle)
+            attempts.append({"transport": kind, "result": "setup"})
+            continue
+        for f in schedules:
+            try:
+                good = selftest(kind, handle, f)
+            except Exception as e:  # noqa: BLE001 - e.g. the gated grid refused, a timed-out wait
+                print(f"{who}: native {kind} self-test raised ({e})", flush=True)
+                good = False
+            if agree(good):
+                attempts.append({"transport": kind, "result": "ok", "fused": f})
+                return kind, handle, f, attempts
+        attempts.append({"transport": kind, "result": "selftest"})
+        release(kind, handle)
+    return None, None, False, attempts
 
 
 def native_selftest(sim: "DistHeat", kind: str, handle, fused: bool, n: int = 1024) -> bool:

@@ -169,9 +169,10 @@ def scan(x: torch.Tensor, exclusive: bool = False, out: torch.Tensor | None = No
             _ext.call_hip("cme_scan_rts", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype], int(exclusive),
                           workspace(x.device, 8192, "rts").data_ptr(), s)
         elif algo in ("blelloch", "hillis"):
+            # one 4-B sum / prefix per 4096-element tile
+            ws = workspace(x.device, 4 * ((n + 4095) // 4096) + 256, "tree")
             _ext.call_hip("cme_scan_tree", x.data_ptr(), out.data_ptr(), n, _DT_SCAN[x.dtype],
-                          0 if algo == "blelloch" else 1, int(exclusive), workspace(x.device, 8192, "rts").data_ptr(),
-                          s)
+                          0 if algo == "blelloch" else 1, int(exclusive), ws.data_ptr(), s)
         elif algo in ("blelloch_mlevel", "hillis_mlevel"):
             if out.data_ptr() == x.data_ptr() and not exclusive:
                 raise ValueError("in-place inclusive multi-level scan is not supported")

@@ -5,6 +5,7 @@ stencil's K-step loop runs entirely in ``cme_heat_dist_run``)."""
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -30,6 +31,10 @@ class NativeRccl:
             raise RuntimeError("torch.distributed must be initialised first")
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
+        if os.environ.get("CME_FAULT_RCCL_INIT", "0") not in ("", "0"):
+            # fault injection (tests of the transport chain): every rank that
+            # sees it fails here, before the collective ncclCommInitRank
+            raise RuntimeError("RCCL init failed (CME_FAULT_RCCL_INIT)")
         dev = torch.device("cuda", torch.cuda.current_device())
         uid = torch.zeros(128, dtype=torch.uint8)
         if self.rank == 0:

@@ -341,9 +341,10 @@ def main() -> int:
     ap.add_argument("--schedule", choices=["auto", "events"], default="auto",
                     help="native loop: auto = fused one-launch passes where the native loop allows them (falls back "
                          "to events if the self-test fails); events = schedule 0 (border / comm / interior streams)")
-    ap.add_argument("--transport", choices=["rccl", "ipc"], default="rccl",
+    ap.add_argument("--transport", choices=["auto", "rccl", "ipc", "rccl,ipc"], default="auto",
                     help="native halo transport: rccl = grouped ncclSend/Recv; ipc = peers' memory mapped "
-                         "with hipIpcOpenMemHandle, pulled by a kernel over xGMI")
+                         "with hipIpcOpenMemHandle, pulled by a kernel over xGMI; auto = rccl, then ipc if RCCL "
+                         "fails its setup or bitwise self-test, then the torch.distributed loop")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = dry run of the multi-rank control flow on gloo + the OpenMP backend "
                          "(tests; never the reported number)")
@@ -406,7 +407,8 @@ def main() -> int:
     # schedule 0 if that fails); every rank agrees, "auto" falls back to the
     # torch.distributed loop, "on" raises
     try:
-        info = sim.enable_native(args.transport if not args.share_gpu else "ipc", fused=args.schedule == "auto")
+        info = sim.enable_native("ipc" if args.share_gpu else (None if args.transport == "auto" else args.transport),
+                                 fused=args.schedule == "auto")
     except RuntimeError as e:
         print(f"bench.py: --native on but the native loop failed ({e})", file=sys.stderr)
         return 3
@@ -634,6 +636,8 @@ def main() -> int:
                                                                             else "single (native multi-pass)"),
                 "transport": (info["transport"] if use_native else ("torch.distributed" if comm.size > 1 else "none")),
                 "schedule": schedule,
+                # the native transport chain as tried (rccl -> ipc -> torch.distributed loop)
+                "transport_attempts": info.get("attempts", []),
             },
             "hbm_GBps_min_traffic": round(hbm, 1),
             "pct_peak_hbm_per_gpu": round(100.0 * hbm / args.gpus / 8000.0, 1),

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kernel", default="streamn", choices=["streamn", "pipe"],
                     help="3-4 step pass kernel: streamN or the wave-pipelined pass")
+    ap.add_argument("--sync", action="store_true",
+                    help="sync mode: exchange, then every row of the subdomain in one region (no separate border "
+                         "strips; with the no-op exchange this bounds what folding the borders in can gain)")
     ap.add_argument("--tune", nargs="*", default=[],
                     help="tuning knobs name=value (cme213x.utils.tuning), e.g. pipe_per_cu=6 pipe_vw=4")
     args = ap.parse_args()
@@ -63,7 +66,7 @@ def main():
     base = None
     for w in args.world:
         rank = w // 2 if w > 1 else 0  # an inner rank: two neighbours
-        p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=False, flavor="hw5")
+        p = SimParams(nx=args.n, ny=args.n, order=8, grid_method=args.method, sync=args.sync, flavor="hw5")
         arith = args.arith or ("fma" if args.fma else "exact")
         fma_arg = {"exact": False, "fma": True, "fast": "fast"}[arith]
         sim = DistHeat(p, NullComm(rank, w), torch.float32, "cuda", tblock=args.tblock, fma=fma_arg,
@@ -87,7 +90,8 @@ def main():
             times.append(e0.elapsed_time(e1) / args.steps)
         ms = sorted(times)[len(times) // 2]
         base = base or ms * w
-        print(json.dumps({"world": w, "rank": rank, "method": args.method, "native": args.native, "tblock": args.tblock,
+        print(json.dumps({"world": w, "rank": rank, "method": args.method, "sync": args.sync, "native": args.native,
+                          "tblock": args.tblock,
                           "arith": arith,
                           "kernel": args.kernel, "tune": knobs,
                           "reps": args.reps,

@@ -54,8 +54,9 @@ CME_EXPORT int cme_scan_rts(const void* in, void* out, long long n, int dtype, i
     }
 }
 
-// Reduce-then-scan with a tree block scan: algo 0 Blelloch, 1 Hillis-Steele.
-// ws: >= 4 * 1024 bytes.
+// Tile-parallel reduce-then-scan with a tree block scan (scan_kernels.h
+// launch_tree_rts): algo 0 Blelloch, 1 Hillis-Steele. ws: >= 4 * ceil(n / 4096)
+// bytes (the tile sums, then their prefixes).
 CME_EXPORT int cme_scan_tree(const void* in, void* out, long long n, int dtype, int algo, int exclusive, void* ws,
                              void* stream) {
     hipStream_t s = as_stream(stream);
@@ -222,5 +223,5 @@ CME_REGISTER_KERNEL(scan_lookback_f32, 256,
                     scan_lookback_kernel<float, true, kLbRows, true, kLbMode, false, kLbPf, kLbNt>);
 CME_REGISTER_KERNEL(scan_rts_reduce_f32, 256, rts_reduce_kernel<float>);
 CME_REGISTER_KERNEL(scan_rts_scan_f32, 256, rts_scan_kernel<float, true>);
-CME_REGISTER_KERNEL(scan_blelloch_rts_f32, 256, rts_tree_scan_kernel<float, true, 0>);
+CME_REGISTER_KERNEL(scan_blelloch_rts_f32, 256, tile_tree_scan_kernel<float, true, 0>);
 CME_REGISTER_KERNEL(segscan_bitmask_fused, 256, segscan_kernel<1, true, 4, false, true>);

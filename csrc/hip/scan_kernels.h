@@ -501,30 +501,67 @@ __device__ __forceinline__ T tree_block_exclusive(T v, T* s, T* s2, T& total) {
 // conflicts in the thread-contiguous reads / writes)
 __host__ __device__ constexpr int tpad(int i) { return i + (i >> 4); }
 
+// Tile-parallel reduce-then-scan with the lecture's tree at the block level.
+//  K1 tile_reduce_kernel: one sum per 4096-element tile (16 B loads, the next
+//     tile prefetched), tiles visited in ascending order (iteration j of the
+//     grid-stride loop covers tiles [jG, (j+1)G));
+//  K2 rts_partials_kernel: exclusive scan of the tile sums (one block);
+//  K3 tile_tree_scan_kernel: each tile independently -- coalesced 16-B loads
+//     staged through LDS, 16 consecutive values per thread scanned in
+//     registers, the 256 thread totals by the block tree (Blelloch / Hillis),
+//     plus the tile's prefix from K2 -- visiting the tiles in DESCENDING
+//     order, so the first tiles K3 reads are the last K1 read, still in the
+//     256 MB Infinity Cache (every 2^26 fp32 tile but the first ~13 MB of K1's
+//     sweep), and storing non-temporally (the output is written once).
+// 12 B per element from HBM at most (my-refs/scan.pdf: reduce, scan of block
+// sums, scan + add), bitwise reproducible (fixed trees, no hand-off).
+template <typename T>
+__device__ __forceinline__ void tile_load4(const T* __restrict__ in, long long t0, long long n, Vec4<T> (&q)[4]) {
+#pragma unroll
+    for (int k = 0; k < kTreeTile / 1024; ++k) q[k] = load_v4(in, t0 + k * 1024 + (int)threadIdx.x * 4, n, T(0));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void tile_reduce_kernel(const T* __restrict__ in, long long n, int ntiles,
+                                                          T* __restrict__ tsum) {
+    __shared__ T lds[4];
+    Vec4<T> q[4], qn[4];
+    int tile = blockIdx.x;
+    if (tile < ntiles) tile_load4(in, (long long)tile * kTreeTile, n, q);
+    for (; tile < ntiles; tile += gridDim.x) {
+        if (tile + (int)gridDim.x < ntiles) tile_load4(in, (long long)(tile + gridDim.x) * kTreeTile, n, qn);
+        T acc = T(0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = acc + ((q[k].x + q[k].y) + (q[k].z + q[k].w));
+        const T r = block_reduce<4>(acc, lds, OpAdd());
+        if (threadIdx.x == 0) tsum[tile] = r;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = qn[k];
+    }
+}
+
 template <typename T, bool EXCLUSIVE, int ALGO>
-__global__ __launch_bounds__(256) void rts_tree_scan_kernel(const T* __restrict__ in, T* __restrict__ out, long long n,
-                                                            long long chunk, const T* __restrict__ part) {
+__global__ __launch_bounds__(256) void tile_tree_scan_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                             long long n, int ntiles, const T* __restrict__ tpre) {
     __shared__ T s[4 * (kWave + kWave / 32) + 4];  // Blelloch: 4 padded wave segments + the wave totals
     __shared__ T s2[ALGO == 1 ? 256 : 1];
-    // The tree wants 16 CONSECUTIVE values per thread; read that way from
-    // memory, a wave's 16-B loads sit 64 B apart (32 lines per instruction),
-    // and the pass ran at 117 us for 2^26 floats against 83 for the DPP block
-    // scan. Tiles move through LDS instead: coalesced 16-B loads and stores
-    // (lane-contiguous, 1 KB per wave instruction), thread-contiguous LDS.
     __shared__ T tile[tpad(kTreeTile)];
     const int t = threadIdx.x;
-    const long long b0 = (long long)blockIdx.x * chunk;
-    const long long b1 = b0 + chunk < n ? b0 + chunk : n;
-    T carry = part[blockIdx.x];
-    for (long long t0 = b0; t0 < b1; t0 += kTreeTile) {
+    Vec4<T> q[4], qn[4];
+    int j = blockIdx.x;  // tile ntiles - 1 - j
+    if (j < ntiles) tile_load4(in, (long long)(ntiles - 1 - j) * kTreeTile, n, q);
+    for (; j < ntiles; j += gridDim.x) {
+        const int id = ntiles - 1 - j;
+        const long long t0 = (long long)id * kTreeTile;
+        const T tile_pre = tpre[id];
+        if (j + (int)gridDim.x < ntiles) tile_load4(in, (long long)(id - (int)gridDim.x) * kTreeTile, n, qn);
 #pragma unroll
-        for (int k = 0; k < kTreeTile / 1024; ++k) {
+        for (int k = 0; k < 4; ++k) {
             const int e = k * 1024 + t * 4;
-            const Vec4<T> q = load_v4(in, t0 + e, b1, T(0));
-            tile[tpad(e)] = q.x;
-            tile[tpad(e + 1)] = q.y;
-            tile[tpad(e + 2)] = q.z;
-            tile[tpad(e + 3)] = q.w;
+            tile[tpad(e)] = q[k].x;
+            tile[tpad(e + 1)] = q[k].y;
+            tile[tpad(e + 2)] = q[k].z;
+            tile[tpad(e + 3)] = q[k].w;
         }
         __syncthreads();
         T v[kTreeItems];
@@ -540,33 +577,42 @@ __global__ __launch_bounds__(256) void rts_tree_scan_kernel(const T* __restrict_
         T tot;
         // (its barriers also order every thread's reads above before the
         // writes below)
-        const T pre = carry + tree_block_exclusive<T, ALGO>(acc, s, s2, tot);
+        const T pre = tile_pre + tree_block_exclusive<T, ALGO>(acc, s, s2, tot);
 #pragma unroll
         for (int k = 0; k < kTreeItems; ++k) tile[tpad(t * kTreeItems + k)] = pre + v[k];
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kTreeTile / 1024; ++k) {
+        for (int k = 0; k < 4; ++k) {
             const int e = k * 1024 + t * 4;
+            const long long oi = t0 + e;
             const Vec4<T> r{tile[tpad(e)], tile[tpad(e + 1)], tile[tpad(e + 2)], tile[tpad(e + 3)]};
-            store_v4(out, t0 + e, b1, r);
+            if (oi + 4 <= n) {
+                typedef T v4 __attribute__((ext_vector_type(4)));
+                const v4 o = {r.x, r.y, r.z, r.w};
+                __builtin_nontemporal_store(o, reinterpret_cast<v4*>(out + oi));
+            } else {
+                store_v4(out, oi, n, r);
+            }
         }
         __syncthreads();  // the next tile's staging writes
-        carry = carry + tot;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = qn[k];
     }
 }
 
+// ws: 4-B tile sums / prefixes, cdiv(n, 4096) of them
 template <typename T>
 int launch_tree_rts(const T* in, T* out, long long n, int algo, int exclusive, void* ws, hipStream_t s) {
     if (n <= 0) return 0;
     const long long tiles = (n + kTreeTile - 1) / kTreeTile;
-    int blocks = tiles < kRtsBlocks ? (int)tiles : kRtsBlocks;
-    const long long chunk = ((tiles + blocks - 1) / blocks) * kTreeTile;
-    blocks = (int)((n + chunk - 1) / chunk);
+    if (tiles >= (1ll << 31)) return (int)hipErrorInvalidValue;
+    const int nt = (int)tiles;
+    const int blocks = nt < kRtsBlocks ? nt : kRtsBlocks;
     T* part = (T*)ws;
-    hipLaunchKernelGGL(rts_reduce_kernel<T>, dim3(blocks), dim3(256), 0, s, in, n, chunk, part);
-    hipLaunchKernelGGL(rts_partials_kernel<T>, dim3(1), dim3(1024), 0, s, part, blocks);
+    hipLaunchKernelGGL(tile_reduce_kernel<T>, dim3(blocks), dim3(256), 0, s, in, n, nt, part);
+    hipLaunchKernelGGL(rts_partials_kernel<T>, dim3(1), dim3(1024), 0, s, part, nt);
 #define TREE(E, A) \
-    hipLaunchKernelGGL((rts_tree_scan_kernel<T, E, A>), dim3(blocks), dim3(256), 0, s, in, out, n, chunk, part)
+    hipLaunchKernelGGL((tile_tree_scan_kernel<T, E, A>), dim3(blocks), dim3(256), 0, s, in, out, n, nt, part)
     if (algo == 0) {
         if (exclusive) TREE(true, 0); else TREE(false, 0);
     } else {

@@ -358,3 +358,68 @@ def test_native_setup_every_rank_falls_back_together(fail_rank, fail_step):
     assert parts[0][1] == parts[1][1]  # same number of agree() calls on both ranks
     if fail_step == "lib":
         assert all(p[2] == 0 for p in parts)  # nobody opened a transport
+
+
+def _chain_rank(rank, world, scenario):
+    """The native transport chain (RCCL -> IPC -> Python loop) with faked
+    transports: which kind every rank ends on, and its agreement count."""
+    import torch.distributed as dist
+
+    from cme213x.models.heat2d_dist import choose_native_transport
+
+    calls, released = [], []
+
+    def agree(ok):
+        calls.append(ok)
+        t = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item() == 1.0)
+
+    def open_transport(kind):
+        if kind == "rccl" and scenario == "rccl_setup" and rank == 1:
+            raise RuntimeError("faked ncclCommInitRank failure")
+        if scenario == "all_setup":
+            raise RuntimeError("faked transport failure")
+        return f"{kind}-handle"
+
+    def selftest(kind, handle, fused):
+        if scenario == "rccl_selftest" and kind == "rccl" and rank == 0:
+            return False
+        if scenario == "ipc_fused" and kind == "ipc" and fused and rank == 1:
+            raise TimeoutError("faked gate timeout")
+        return True
+
+    def release(kind, handle):
+        released.append(kind)
+
+    kind, handle, fused, attempts = choose_native_transport(["rccl", "ipc"], agree, lambda: None, open_transport,
+                                                            selftest, release, (True, False), f"rank {rank}")
+    t = torch.tensor([float(len(calls))])
+    dist.all_reduce(t)  # a rank left alone in a collective would hang here
+    return kind, handle, fused, attempts, len(calls), released
+
+
+@pytest.mark.parametrize("scenario,want,fused", [("none", "rccl", True), ("rccl_setup", "ipc", True),
+                                                 ("rccl_selftest", "ipc", True), ("ipc_fused", "rccl", True),
+                                                 ("all_setup", None, False)])
+def test_native_transport_chain_gloo(scenario, want, fused):
+    """RCCL failing its setup (on one rank) or its bitwise
+    self-test moves EVERY rank to the IPC transport together, with the same
+    number of agreement collectives; a failed self-test releases the RCCL
+    handle first; with no transport left every rank ends on the Python
+    loop. (ipc_fused: RCCL passes, so IPC is never tried.)"""
+    parts = run_ranks(_chain_rank, 2, (scenario,))
+    kinds = {p[0] for p in parts}
+    assert kinds == {want}, parts
+    assert parts[0][4] == parts[1][4]  # same number of agree() calls
+    assert parts[0][3] == parts[1][3]  # same attempt record on every rank
+    assert parts[0][2] == fused
+    if scenario == "rccl_setup":
+        assert [a["result"] for a in parts[0][3]] == ["setup", "ok"]
+        assert parts[0][1] == "ipc-handle"
+        assert parts[0][5] == ["rccl"] and parts[1][5] == []  # rank 0's opened communicator aborted
+    if scenario == "rccl_selftest":
+        assert [a["result"] for a in parts[0][3]] == ["selftest", "ok"]
+        assert all(p[5] == ["rccl"] for p in parts)  # RCCL released on both ranks before IPC opened
+    if scenario == "all_setup":
+        assert [a["result"] for a in parts[0][3]] == ["setup", "setup"]

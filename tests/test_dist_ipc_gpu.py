@@ -249,3 +249,53 @@ def test_ipc_eight_processes_driver_plan(gpu):
         want = st[B + y0:B + y0 + own.shape[0], B + x0:B + x0 + own.shape[1]]
         assert np.array_equal(own, want), f"rank {r} ({sch}): max |diff| {np.abs(own - want).max()}"
         assert sch["schedule"] == "fused" and sch["probe"] == "passed", sch
+
+
+def _chain_rank(rank, world):
+    """RCCL fails its setup on every rank (fault injection before the
+    collective ncclCommInitRank); the chain must land on IPC."""
+    import os
+
+    import torch
+
+    os.environ["CME_FAULT_RCCL_INIT"] = "1"
+    import cme213x  # noqa: F401
+    from cme213x.models.heat2d_dist import DistHeat
+    from cme213x.parallel.comm import TorchComm
+
+    torch.cuda.set_device(0)
+    comm = TorchComm()
+    p = _params(1, False)
+    sim = DistHeat(p, comm, torch.float32, "cuda:0", tblock=4, fma=True, kernel="pipe", native="on")
+    info = sim.enable_native("rccl,ipc")
+    _set_ic(sim, torch.float32)
+    sim.run(p.iters)
+    sim.check_native()
+    s = next(iter(sim.subs.values()))
+    H = s.grid.H
+    own = s.grid.buf[s.grid.cur, H:H + s.blk.ny, H:H + s.blk.nx].cpu().numpy()
+    sim.close_native()
+    return s.blk.x0, s.blk.y0, own, info
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_transport_chain_falls_back_to_ipc(gpu):
+    """with RCCL failing on every rank, enable_native's chain
+    (rccl -> ipc -> Python loop) runs the native loop over IPC on all ranks,
+    bitwise equal to the single-grid oracle (2 processes on one GPU, fused
+    4-step pipelined passes)."""
+    from cme213x.models.heat2d_dist import DistHeat
+
+    parts = run_ranks(_chain_rank, 2, (), timeout=240)
+    p = _params(1, False)
+    ref = DistHeat(p, None, torch.float32, "cpu", variant="naive", fma=True)
+    _set_ic(ref, torch.float32)
+    ref.run(p.iters)
+    st = ref.gather_global()
+    B = p.border
+    for r, (x0, y0, own, info) in enumerate(parts):
+        assert info["loop"] == "native" and info["transport"] == "ipc", info
+        assert [a["result"] for a in info["attempts"]] == ["setup", "ok"], info
+        want = st[B + y0:B + y0 + own.shape[0], B + x0:B + x0 + own.shape[1]]
+        assert np.array_equal(own.astype(np.float64), want), f"rank {r}: max |diff| {np.abs(own - want).max()}"
