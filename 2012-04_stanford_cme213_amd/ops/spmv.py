@@ -40,8 +40,16 @@ class CSR:
     def nnz(self) -> int:
         return self.col.numel()
 
+    def __post_init__(self):
+        # host row pointers: cache the longest row now (spmv "auto" reads it,
+        # and a stream capture cannot compute it)
+        if not self.rp.is_cuda:
+            max_row_length(self)
+
     def to(self, device) -> "CSR":
-        return CSR(self.nrows, self.ncols, self.rp.to(device), self.col.to(device), self.val.to(device))
+        out = CSR(self.nrows, self.ncols, self.rp.to(device), self.col.to(device), self.val.to(device))
+        _carry_max_row(self, out)
+        return out
 
     def to_dense(self) -> torch.Tensor:
         rows = torch.repeat_interleave(torch.arange(self.nrows), torch.diff(self.rp.cpu().long()))
@@ -341,17 +349,30 @@ SCALAR_MAX_MEAN, SCALAR_MAX_ROW = 8, 16
 _MAX_ROW: dict = {}
 
 
+def _cache_max_row(rp: torch.Tensor, v: int) -> None:
+    key = id(rp)
+    _MAX_ROW[key] = (weakref.ref(rp, lambda _r, k=key: _MAX_ROW.pop(k, None)), rp._version, v)
+
+
+def _carry_max_row(src: CSR, dst: CSR) -> None:
+    """dst holds src's rows on another device: the cached longest row moves
+    with them (computed on the source if need be)."""
+    v = max_row_length(src)
+    if v is not None:
+        _cache_max_row(dst.rp, v)
+
+
 def max_row_length(a: CSR) -> int | None:
-    """Longest row of ``a`` (cached per row-pointer tensor; None while a
-    stream is being captured and the value is not cached yet)."""
+    """Longest row of ``a`` (cached per row-pointer tensor: a CSR built on the
+    host caches it at construction and carries it through ``.to()``; None
+    only for device row pointers first seen during a stream capture)."""
     hit = _MAX_ROW.get(id(a.rp))
     if hit is not None and hit[0]() is a.rp and hit[1] == a.rp._version:
         return hit[2]
     if a.rp.is_cuda and torch.cuda.is_current_stream_capturing():
         return None
     v = int(torch.diff(a.rp).max().item()) if a.nrows > 0 else 0
-    key = id(a.rp)
-    _MAX_ROW[key] = (weakref.ref(a.rp, lambda _r, k=key: _MAX_ROW.pop(k, None)), a.rp._version, v)
+    _cache_max_row(a.rp, v)
     return v
 
 
@@ -368,6 +389,17 @@ def short_rows_per_lane(a: CSR) -> int:
 
     r = tuning.get("spmv_short_rpt") if a.rp.is_cuda else 1
     return r if r in (1, 2, 4) else 1
+
+
+def _auto_max_row(a: CSR) -> int:
+    """The longest row for the CSR "auto" choice; refuses (instead of
+    silently choosing another kernel than eager mode would) when a capture
+    meets device row pointers whose longest row was never computed."""
+    v = max_row_length(a)
+    if v is None:
+        raise RuntimeError("spmv(kernel='auto') under stream capture: the longest row of this CSR is unknown -- "
+                           "build it on the host and move it with .to(), or call spmv once before capturing")
+    return v
 
 
 def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto", beta: float = 0.0) -> torch.Tensor:
@@ -397,7 +429,7 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
         _ext.call_hip("cme_spmv_csr_aligned", a.nrows, a.nnz, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), g, float(beta), s)
     elif isinstance(a, CSR) and kernel == "auto" and a.nnz <= SCALAR_MAX_MEAN * max(1, a.nrows) and \
-            (max_row_length(a) or SCALAR_MAX_ROW + 1) <= SCALAR_MAX_ROW:
+            _auto_max_row(a) <= SCALAR_MAX_ROW:
         _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
                       y.data_ptr(), 1, float(beta), s)
     elif isinstance(a, CSR) and kernel == "short":

@@ -14,15 +14,18 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=1 << 26)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--algos", nargs="*", default=["lookback", "rts", "blelloch", "hillis"])
+    ap.add_argument("--sets", type=int, default=1,
+                    help="operand sets visited round-robin (3: every call cold, as bench.py's config #3)")
     a = ap.parse_args()
     import torch
 
     from cme213x.ops.scan import scan
 
-    x = (torch.rand(a.n, device="cuda") < 0.2).float()
+    xs = [torch.rand(a.n, device="cuda") for _ in range(a.sets)]
+    ys = [torch.empty_like(x) for x in xs]
     for algo in a.algos:
-        for _ in range(a.reps):
-            scan(x, True, algo=algo)
+        for i in range(a.reps):
+            scan(xs[i % a.sets], True, ys[i % a.sets], algo=algo)
     torch.cuda.synchronize()
     print("done", flush=True)
     return 0

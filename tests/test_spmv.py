@@ -214,3 +214,40 @@ def test_csr_auto_kernel_rule():
     assert stream_rows(random_csr(1000, 1000, 8, seed=1)) == 256
     assert stream_rows(random_csr(1000, 1000, 14, seed=1)) == 128
     assert stream_rows(random_csr(1000, 1000, 30, seed=1)) == 64
+
+
+def test_csr_caches_longest_row_at_build_and_to():
+    """a host-built CSR knows its longest row before any capture,
+    and .to() carries it to the new row pointers."""
+    from cme213x.ops.spmv import _MAX_ROW, laplacian
+
+    a = laplacian("5pt", 30)
+    assert id(a.rp) in _MAX_ROW and _MAX_ROW[id(a.rp)][2] == 5
+    b = a.to("cpu")
+    assert id(b.rp) in _MAX_ROW and _MAX_ROW[id(b.rp)][2] == 5
+
+
+@pytest.mark.gpu
+def test_csr_auto_graph_equals_eager(gpu):
+    """The captured graph takes the same "auto" kernel as eager mode (bitwise
+    equal outputs); a device-built CSR whose longest row is unknown refuses
+    to be captured instead of silently switching kernels."""
+    import torch
+
+    from cme213x.ops.spmv import CSR, laplacian, spmv
+
+    a = laplacian("5pt", 300).to(gpu)
+    x = torch.rand(a.ncols, device=gpu)
+    eager = spmv(a, x)
+    y = torch.empty(a.nrows, device=gpu)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        spmv(a, x, y)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(eager, y)
+    raw = CSR(a.nrows, a.ncols, a.rp.clone(), a.col, a.val)  # device row pointers, never measured
+    g2 = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="longest row"):
+        with torch.cuda.graph(g2):
+            spmv(raw, x, y)
