@@ -235,16 +235,30 @@ __global__ __launch_bounds__(256) void rts_reduce_kernel(const T* __restrict__ i
     if (threadIdx.x == 0) part[blockIdx.x] = r;
 }
 
+// exclusive scan of m partials in place, one block: 16 consecutive values per
+// thread scanned serially, the 1024 thread totals by the block scan (m =
+// 16384 tile sums of a 2^26 tree scan: one round instead of 16 block scans,
+// 14 -> ~4 us)
 template <typename T>
 __global__ __launch_bounds__(1024) void rts_partials_kernel(T* part, int m) {
+    constexpr int kPer = 16;
     __shared__ T lds[16];
     T carry = T(0);
-    for (int base = 0; base < m; base += 1024) {
-        const int i = base + threadIdx.x;
-        T v = i < m ? part[i] : T(0);
+    for (int base = 0; base < m; base += 1024 * kPer) {
+        const int i0 = base + (int)threadIdx.x * kPer;
+        T v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) v[k] = i0 + k < m ? part[i0 + k] : T(0);
+        T acc = T(0);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) acc = acc + v[k];
         T tot;
-        T ex = block_exclusive_scan<16>(v, lds, tot, OpAdd());
-        if (i < m) part[i] = carry + ex;
+        T run = carry + block_exclusive_scan<16>(acc, lds, tot, OpAdd());
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (i0 + k < m) part[i0 + k] = run;
+            run = run + v[k];
+        }
         carry = carry + tot;
     }
 }
