@@ -235,30 +235,51 @@ __global__ __launch_bounds__(256) void rts_reduce_kernel(const T* __restrict__ i
     if (threadIdx.x == 0) part[blockIdx.x] = r;
 }
 
-// exclusive scan of m partials in place, one block: 16 consecutive values per
-// thread scanned serially, the 1024 thread totals by the block scan (m =
-// 16384 tile sums of a 2^26 tree scan: one round instead of 16 block scans,
-// 14 -> ~4 us)
+// exclusive scan of m partials in place, one block of 1024 threads: 8192
+// values per round staged through LDS with coalesced 16-B loads and stores,
+// 8 consecutive values per thread scanned serially, the 1024 thread totals by
+// the block scan (m = 16384 tile sums of a 2^26 tree scan: 2 rounds; direct
+// thread-contiguous global loads touched 16x the lines and took 17 us)
 template <typename T>
 __global__ __launch_bounds__(1024) void rts_partials_kernel(T* part, int m) {
-    constexpr int kPer = 16;
+    constexpr int kPer = 8, kRound = 1024 * kPer;
     __shared__ T lds[16];
+    __shared__ T stage[kRound + kRound / 16];  // one pad word per 16 (thread runs of 8: conflict-free halves)
+    auto sp = [](int i) { return i + (i >> 4); };
+    const int t = threadIdx.x;
     T carry = T(0);
-    for (int base = 0; base < m; base += 1024 * kPer) {
-        const int i0 = base + (int)threadIdx.x * kPer;
-        T v[kPer];
+    for (int base = 0; base < m; base += kRound) {
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) v[k] = i0 + k < m ? part[i0 + k] : T(0);
+        for (int k = 0; k < kPer / 4; ++k) {
+            const int e = (k * 1024 + t) * 4;
+            const Vec4<T> q = load_v4(part, (long long)base + e, m, T(0));
+            stage[sp(e)] = q.x;
+            stage[sp(e + 1)] = q.y;
+            stage[sp(e + 2)] = q.z;
+            stage[sp(e + 3)] = q.w;
+        }
+        __syncthreads();
+        T v[kPer];
         T acc = T(0);
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) acc = acc + v[k];
+        for (int k = 0; k < kPer; ++k) {
+            v[k] = stage[sp(t * kPer + k)];
+            acc = acc + v[k];
+        }
         T tot;
-        T run = carry + block_exclusive_scan<16>(acc, lds, tot, OpAdd());
+        T run = carry + block_exclusive_scan<16>(acc, lds, tot, OpAdd());  // (its barriers order the reads)
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            if (i0 + k < m) part[i0 + k] = run;
+            stage[sp(t * kPer + k)] = run;
             run = run + v[k];
         }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer / 4; ++k) {
+            const int e = (k * 1024 + t) * 4;
+            store_v4(part, (long long)base + e, m, Vec4<T>{stage[sp(e)], stage[sp(e + 1)], stage[sp(e + 2)], stage[sp(e + 3)]});
+        }
+        __syncthreads();  // the next round's staging writes
         carry = carry + tot;
     }
 }
