@@ -25,6 +25,7 @@ _ext.proto(_ext.CPU_PROTOS, "cme_cpu_spmv_csr", "ipppppf")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_aligned", "iqpppppifp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_stream", "ipppppifp")
 _ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_short", "ipppppifp")
+_ext.proto(_ext.HIP_PROTOS, "cme_spmv_csr_wave", "ipppppfp")
 
 
 # ---------------------------------------------------------------- formats
@@ -432,6 +433,9 @@ def spmv(a, x: torch.Tensor, y: torch.Tensor | None = None, kernel: str = "auto"
             _auto_max_row(a) <= SCALAR_MAX_ROW:
         _ext.call_hip("cme_spmv_csr", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(), x.data_ptr(),
                       y.data_ptr(), 1, float(beta), s)
+    elif isinstance(a, CSR) and kernel == "wave":
+        _ext.call_hip("cme_spmv_csr_wave", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
+                      x.data_ptr(), y.data_ptr(), float(beta), s)
     elif isinstance(a, CSR) and kernel == "short":
         _ext.call_hip("cme_spmv_csr_short", a.nrows, a.rp.data_ptr(), a.col.data_ptr(), a.val.data_ptr(),
                       x.data_ptr(), y.data_ptr(), short_rows_per_lane(a), float(beta), s)
@@ -541,7 +545,7 @@ def prepare(a: CSR, fmt: str = "auto", device=None):
         m = to_csr_colblocked(a, int(parts[0]) << 10, aligned=not (len(parts) > 1 and parts[1] == "u"))
         return fmt, (m.to(device) if device is not None else m)
     conv = {"csr": lambda m: m, "csr_scalar": lambda m: m, "csr_vector": lambda m: m, "csr_stream": lambda m: m,
-            "csr_short": lambda m: m,
+            "csr_short": lambda m: m, "csr_wave": lambda m: m,
             "csr_aligned": to_csr_aligned,
             "csr_cb": to_csr_colblocked,
             "coo": to_coo, "hyb": to_hyb, "dia": to_dia, "ell": lambda m: to_ell(m)[0]}

@@ -132,7 +132,7 @@ def main():
                 continue
             if f == "dia" and (st.ndiag > 64 or st.dia_fill < 0.3):
                 continue
-            if f in ("csr_scalar", "csr_short") and st.max_row > 1024:
+            if f in ("csr_scalar", "csr_short", "csr_wave") and st.max_row > 1024:
                 continue  # thread-per-row on a power-law row: seconds, not a contender
             _, m = prepare(A, f, "cuda")
             mb = nbytes(m) + 4 * (A.ncols + A.nrows)
@@ -140,7 +140,8 @@ def main():
             sets = [(m, torch.rand(A.ncols, device="cuda"), torch.empty(A.nrows, device="cuda"))]
             for _ in range(reps - 1):
                 sets.append((clone(m), torch.rand(A.ncols, device="cuda"), torch.empty(A.nrows, device="cuda")))
-            kern = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream", "csr_short": "short"}.get(f, "auto")
+            kern = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream", "csr_short": "short",
+                    "csr_wave": "wave"}.get(f, "auto")
 
             def cold():
                 for i in range(args.calls):

@@ -267,6 +267,57 @@ __global__ __launch_bounds__(256) void csr_short_kernel(int nrows, const int* __
     }
 }
 
+// CSR-wave (short rows, config #4's 5-point Laplacian): one wave per 64
+// consecutive rows and no workgroup barrier. The wave's nonzero range
+// [rp[r0], rp[r0 + 64]) is contiguous in col / val, so its lanes stream it
+// with coalesced loads (entry s + lane + 64 q: every load instruction carries
+// 64 useful consecutive entries, against csr_scalar's 64 rows x 20-B stride,
+// ~10 lines per instruction, re-touched by each of a row's loads), gather x
+// for each entry and leave the PRODUCT in the wave's LDS slice; then lane l
+// sums its row's products out of the slice in entry order. The slice is the
+// wave's own (wave_lds_sync: in-wave ordering). A wave whose range exceeds the
+// slice takes the lane-per-row loop over global memory.
+constexpr int kWaveCap = 1024;  // products per wave: 4 KB, 16 KB per 256-lane workgroup
+
+__global__ __launch_bounds__(256) void csr_wave_kernel(int nrows, const int* __restrict__ rp,
+                                                       const int* __restrict__ col, const float* __restrict__ val,
+                                                       const float* __restrict__ x, float* __restrict__ y,
+                                                       float beta) {
+    __shared__ float prod[4][kWaveCap];
+    const int lane = lane_id(), w = (int)(threadIdx.x / kWave);
+    const int r0 = (blockIdx.x * 4 + w) * kWave;
+    if (r0 >= nrows) return;  // wave-uniform; no workgroup barrier below
+    const int r = r0 + lane;
+    const bool valid = r < nrows;
+    const int b = valid ? rp[r] : 0;
+    const int e = valid ? rp[r + 1] : 0;
+    const int rl = r0 + kWave < nrows ? r0 + kWave : nrows;
+    const int s0 = __builtin_amdgcn_readfirstlane(b);  // lane 0 is valid: rp[r0]
+    const int cnt = __builtin_amdgcn_readfirstlane(rp[rl]) - s0;
+    float acc = 0.f;
+    if (cnt <= kWaveCap) {
+        float* pw = prod[w];
+        int q = lane;
+        for (; q + 3 * kWave < cnt; q += 4 * kWave) {  // 4 col / val pairs in flight, then 4 gathers
+            int c[4];
+            float v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                c[k] = col[s0 + q + k * kWave];
+                v[k] = val[s0 + q + k * kWave];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) pw[q + k * kWave] = v[k] * x[c[k]];
+        }
+        for (; q < cnt; q += kWave) pw[q] = val[s0 + q] * x[col[s0 + q]];
+        wave_lds_sync();
+        for (int j = b - s0; j < e - s0; ++j) acc += pw[j];
+    } else {
+        for (int j = b; j < e; ++j) acc += val[j] * x[col[j]];
+    }
+    if (valid) y[r] = beta == 0.f ? acc : beta * y[r] + acc;
+}
+
 // All column / value loads of a group of 4 entries are issued before the
 // dependent x gathers (the row loop is a load-latency chain otherwise);
 // padding (col < 0) is masked without a branch. Summation order is k order.
@@ -480,6 +531,15 @@ CME_EXPORT int cme_spmv_csr_stream(int nrows, const int* rp, const int* col, con
 #undef V
         default: return (int)hipErrorInvalidValue;
     }
+    CME_LAUNCH_STATUS();
+}
+
+// CSR-wave: one wave per 64 rows (csr_wave_kernel).
+CME_EXPORT int cme_spmv_csr_wave(int nrows, const int* rp, const int* col, const float* val, const float* x, float* y,
+                                 float beta, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (nrows <= 0) return 0;
+    hipLaunchKernelGGL(csr_wave_kernel, dim3(cdiv(nrows, 256)), dim3(256), 0, s, nrows, rp, col, val, x, y, beta);
     CME_LAUNCH_STATUS();
 }
 

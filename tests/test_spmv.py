@@ -42,7 +42,8 @@ def test_csr_cpu_and_conversions():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mat", ["5pt", "27pt", "random", "skew"])
-@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_stream", "csr_short", "csr_auto", "csr_aligned", "ell",
+@pytest.mark.parametrize("fmt", ["csr_scalar", "csr_vector", "csr_stream", "csr_short", "csr_wave", "csr_auto",
+                                 "csr_aligned", "ell",
                                  "dia", "coo",
                                  "hyb", "csr_cb"])
 def test_spmv_gpu(gpu, mat, fmt):
@@ -67,12 +68,12 @@ def test_spmv_gpu(gpu, mat, fmt):
         y1 = spmv(dev, x.to(gpu), y0.clone(), beta=0.5).cpu().numpy()
         np.testing.assert_allclose(y1, ref + 0.5 * y0.cpu().numpy(), rtol=1e-4, atol=1e-3)
         return
-    dev = {"csr_scalar": a, "csr_vector": a, "csr_stream": a, "csr_short": a, "csr_auto": a,
+    dev = {"csr_scalar": a, "csr_vector": a, "csr_stream": a, "csr_short": a, "csr_wave": a, "csr_auto": a,
            "csr_aligned": to_csr_aligned(a) if fmt == "csr_aligned" else None,
            "ell": to_ell(a)[0], "dia": to_dia(a) if fmt == "dia" else None,
            "coo": to_coo(a), "hyb": to_hyb(a)}[fmt].to(gpu)
-    kernel = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream", "csr_short": "short"}.get(fmt,
-                                                                                                           "auto")
+    kernel = {"csr_scalar": "scalar", "csr_vector": "vector", "csr_stream": "stream", "csr_short": "short",
+              "csr_wave": "wave"}.get(fmt, "auto")
     y = spmv(dev, x.to(gpu), kernel=kernel).cpu().numpy()
     np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-3)
     # beta accumulate
@@ -146,7 +147,7 @@ def test_colblocked_needs_far_gathers():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows_case", ["long_rows", "empty_rows", "tail", "mixed"])
-@pytest.mark.parametrize("kernel,rpt", [("stream", 0), ("short", 1), ("short", 2), ("short", 4)])
+@pytest.mark.parametrize("kernel,rpt", [("stream", 0), ("short", 1), ("short", 2), ("short", 4), ("wave", 0)])
 def test_spmv_csr_stream_blocks(gpu, rows_case, kernel, rpt):
     """CSR-stream's row blocks: a block whose nonzeros overflow the 4096-
     product LDS buffer takes the wave-per-row fallback (rows of 3000 and 9000
