@@ -115,7 +115,7 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
         v = values.contiguous()
         vout, vtmp = torch.empty_like(v), torch.empty_like(v)
         vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
-    ws = _workspace(keys.device, (k.numel() + 4095) // 4096 * 8 + 256)  # = cme_merge_ws_bytes
+    ws = _workspace(keys.device, (k.numel() + 4095) // 4096 * 16 + 256)  # = cme_merge_ws_bytes
     _ext.call_hip("cme_merge_sort_ws", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
                   _MODES[keys.dtype], ws.data_ptr(), _ext.stream_ptr(keys.device))
     return (out, vout) if values is not None else out

@@ -494,11 +494,21 @@ __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* s
     }
 }
 
-// coalesced tile store through LDS: lane t holds outputs [16t, 16t+16)
+// Run samples of a pass's output for the next pass's partition search: the
+// first and the last key (uint32 codes) of every `st`-key tile of the array.
+struct MsSamples {
+    uint32_t* first;  // nullptr: none written
+    uint32_t* last;
+    int st;
+};
+
+// coalesced tile store through LDS: lane t holds outputs [16t, 16t+16); also
+// records the tile's samples (smp.first != nullptr, block-uniform)
 template <bool HAS_VALUES, int NT>
 __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const uint32_t (&k)[kMsItems],
                                               const uint32_t (&v)[kMsItems], uint32_t* __restrict__ ko,
-                                              uint32_t* __restrict__ vo, long long base, int cnt, int mode) {
+                                              uint32_t* __restrict__ vo, long long base, int cnt, int mode,
+                                              MsSamples smp) {
     __syncthreads();  // every lane is done reading the tile in LDS
     const int t = threadIdx.x;
 #pragma unroll
@@ -507,6 +517,15 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
         if constexpr (HAS_VALUES) sv[lp(kMsItems * t + q)] = v[q];
     }
     __syncthreads();
+    if (smp.first) {
+        const int nq = (cnt + smp.st - 1) / smp.st;
+        for (int q = t; q < nq; q += NT) {
+            const long long g = base / smp.st + q;
+            const int e = (q + 1) * smp.st < cnt ? (q + 1) * smp.st : cnt;
+            smp.first[g] = sk[lp(q * smp.st)];
+            smp.last[g] = sk[lp(e - 1)];
+        }
+    }
     for (int i = t; i < cnt; i += NT) {
         ko[base + i] = ms_key_out(sk[lp(i)], mode);
         if constexpr (HAS_VALUES) vo[base + i] = sv[lp(i)];
@@ -516,7 +535,7 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
 template <bool HAS_VALUES, int BS = kBsThreads>
 __global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko,
                                                            const uint32_t* __restrict__ vi, uint32_t* __restrict__ vo,
-                                                           long long n, int mode_in, int mode_out) {
+                                                           long long n, int mode_in, int mode_out, MsSamples smp) {
     constexpr int BTILE = BS * kMsItems;
     __shared__ uint32_t sk[lp_size(BTILE) + 1];  // + the merge's out-of-run load slot
     __shared__ uint32_t sv[HAS_VALUES ? lp_size(BTILE) : 1];
@@ -573,7 +592,7 @@ __global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __res
                                diag);
         ms_merge16<HAS_VALUES, BTILE>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
     }
-    ms_store_tile<HAS_VALUES, BS>(sk, sv, k, v, ko, vo, base, cnt, mode_out);
+    ms_store_tile<HAS_VALUES, BS>(sk, sv, k, v, ko, vo, base, cnt, mode_out, smp);
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -614,10 +633,19 @@ __device__ __forceinline__ long long ms_coop_split(const uint32_t* __restrict__ 
 // merge kernel's blocks start on their loads instead of each paying the
 // search's dependent global rounds on its own critical path. G trades rounds
 // (latency) against the lines each round touches (G per array and tile).
+//
+// With the previous kernel's run samples (sfirst / slast: first and last key
+// of every `tile`-key tile) the search first narrows to one tile's width on
+// candidates m = jT only: A[jT] is sfirst of A's tile j, and B[diag-1-jT] is
+// the last key of a B tile (diag, jT and B's start are multiples of T), so
+// those rounds read a 8-byte-per-tile array that stays in L2 instead of
+// scattered lines of the keys. Only the last ~log_G T rounds touch the keys.
 template <int G>
 __global__ __launch_bounds__(256) void ms_partition_kernel(const uint32_t* __restrict__ ki, long long n, long long L,
                                                            long long tile, long long ntiles,
-                                                           long long* __restrict__ split) {
+                                                           long long* __restrict__ split,
+                                                           const uint32_t* __restrict__ sfirst,
+                                                           const uint32_t* __restrict__ slast) {
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "partition group: 4-64 lanes");
     const long long t = ((long long)blockIdx.x * 256 + threadIdx.x) / G;
     const int sub = threadIdx.x % G;
@@ -632,6 +660,28 @@ __global__ __launch_bounds__(256) void ms_partition_kernel(const uint32_t* __res
     const uint32_t* B = ki + a0 + la;
     const long long diag = o0 - a0;
     long long lo = diag - lb > 0 ? diag - lb : 0, hi = diag < la ? diag : la;
+    if (sfirst) {  // kernel-uniform
+        // first j in [jlo, jhi) with Q(jT) false: x lies in ((j-1)T, jT]
+        const long long j0 = (lo + tile - 1) / tile, j1 = (hi + tile - 1) / tile;
+        long long jlo = j0, jhi = j1;
+        const long long ga = a0 / tile, gb = (a0 + la + diag) / tile - 1;  // B[diag-1-jT] ends tile gb - j
+        while (__ballot(jlo < jhi)) {
+            const bool act = jlo < jhi;
+            const long long step = (jhi - jlo + G - 1) / G;
+            const long long j = jlo + (long long)sub * step;
+            const bool q = act && j < jhi && sfirst[ga + j] <= slast[gb - j];
+            const uint64_t fails = (__ballot(!q) >> gshift) & gmask;
+            const int f = fails ? __builtin_ctzll(fails) : G;
+            if (act) {
+                const long long nlo = f == 0 ? jlo : jlo + (long long)(f - 1) * step + 1;
+                const long long jf = jlo + (long long)f * step;
+                jhi = f == G ? jhi : (jf < jhi ? jf : jhi);
+                jlo = nlo;
+            }
+        }
+        if (jlo < j1 && jlo * tile < hi) hi = jlo * tile;
+        if (jlo > j0 && (jlo - 1) * tile + 1 > lo) lo = (jlo - 1) * tile + 1;
+    }
     while (__ballot(lo < hi)) {  // until every group of the wave is done
         const bool act = lo < hi;
         const long long step = (hi - lo + G - 1) / G;
@@ -656,7 +706,7 @@ template <bool HAS_VALUES, int NT = kMsThreads>
 __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko,
                                                            const uint32_t* __restrict__ vi, uint32_t* __restrict__ vo,
                                                            long long n, long long L, int mode_out,
-                                                           const long long* __restrict__ split) {
+                                                           const long long* __restrict__ split, MsSamples smp) {
     constexpr int TILE = NT * kMsItems;
     __shared__ uint32_t sk[lp_size(TILE) + 1];  // + the merge's out-of-run load slot
     __shared__ uint32_t sv[HAS_VALUES ? lp_size(TILE) : 1];
@@ -705,7 +755,7 @@ __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __res
     const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int x) { return sk[lp(na + x)]; }, na, nb, diag_l);
     uint32_t k[kMsItems], v[kMsItems];
     ms_merge16<HAS_VALUES, TILE>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
-    ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out);
+    ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out, smp);
 }
 
 }  // namespace
@@ -912,7 +962,7 @@ CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
 // Stable merge sort of n keys from `in` into `out` (ping-pong through `tmp`;
 // `in` may equal `out`; values optional, likewise). mode: 0 uint32, 1 int32,
 // 2 float32 keys.
-CME_EXPORT long long cme_merge_ws_bytes(long long n) { return (long long)cdiv(n, kMsTile) * 8 + 256; }
+CME_EXPORT long long cme_merge_ws_bytes(long long n) { return (long long)cdiv(n, kMsTile) * 16 + 256; }
 
 // merge-pass output tile (tuning knob merge_tile: 4096 or 8192 keys; 8192
 // needs the partition launch)
@@ -922,7 +972,9 @@ static int merge_tile(bool part) {
 
 // ws (cme_merge_ws_bytes(n) bytes, or nullptr): with it every merge pass
 // first computes all tile partitions in one launch (ms_partition_kernel);
-// without it each merge block searches its own (ms_coop_split).
+// without it each merge block searches its own (ms_coop_split). Layout:
+// split[tiles] (8 B), then the run samples first[tiles] and last[tiles]
+// (4 B each) that every kernel but the last writes for the next partition.
 CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin,
                                  uint32_t* vout, uint32_t* vtmp, long long n, int mode, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -952,18 +1004,28 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     const int mtile = merge_tile(part != 0);
     const unsigned btiles = cdiv(n, btile), tiles = cdiv(n, mtile);
     const int m0 = npass ? 0 : mode;
+    // run samples (knob merge_samples, default on): written by every kernel
+    // whose output a partition launch searches next
+    const bool samples = part != 0 && cme::tune_get(cme::kTuneMergeSamples) != 0;
+    const MsSamples none{nullptr, nullptr, mtile};
+    MsSamples smp = none;
+    if (samples) {
+        uint32_t* sbase = (uint32_t*)((char*)ws + (size_t)cdiv(n, kMsTile) * 8);
+        smp = MsSamples{sbase, sbase + cdiv(n, kMsTile), mtile};
+    }
+    const MsSamples smp0 = npass ? smp : none;
     if (big && vin)
         hipLaunchKernelGGL((ms_block_sort_kernel<true, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s, in,
-                           d0, vin, v0, n, mode, m0);
+                           d0, vin, v0, n, mode, m0, smp0);
     else if (big)
         hipLaunchKernelGGL((ms_block_sort_kernel<false, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s,
-                           in, d0, vin, v0, n, mode, m0);
+                           in, d0, vin, v0, n, mode, m0, smp0);
     else if (vin)
         hipLaunchKernelGGL(ms_block_sort_kernel<true>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode,
-                           m0);
+                           m0, smp0);
     else
         hipLaunchKernelGGL(ms_block_sort_kernel<false>, dim3(btiles), dim3(kBsThreads), 0, s, in, d0, vin, v0, n,
-                           mode, m0);
+                           mode, m0, smp0);
     CME_TRY(hipGetLastError());
     const uint32_t *ki = d0, *vi = v0;
     int p = 0;
@@ -977,7 +1039,7 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
             const dim3 grid(cdiv((long long)tiles * g, 256));
 #define CME_PART(G)                                                                                               \
     hipLaunchKernelGGL(ms_partition_kernel<G>, grid, dim3(256), 0, s, ki, n, L, (long long)mtile, (long long)tiles, \
-                       split)
+                       split, smp.first, smp.last)
             if (g == 4) CME_PART(4);
             else if (g == 8) CME_PART(8);
             else if (g == 16) CME_PART(16);
@@ -986,19 +1048,20 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
 #undef CME_PART
         }
         const int mo = last ? mode : 0;
+        const MsSamples so = last ? none : smp;
         if (mtile == 8192) {
             if (vin)
                 hipLaunchKernelGGL((ms_merge_pass_kernel<true, 512>), dim3(tiles), dim3(512), 0, s, ki, ko, vi, vo, n,
-                                   L, mo, split);
+                                   L, mo, split, so);
             else
                 hipLaunchKernelGGL((ms_merge_pass_kernel<false, 512>), dim3(tiles), dim3(512), 0, s, ki, ko, vi, vo, n,
-                                   L, mo, split);
+                                   L, mo, split, so);
         } else if (vin) {
             hipLaunchKernelGGL(ms_merge_pass_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n, L,
-                               mo, split);
+                               mo, split, so);
         } else {
             hipLaunchKernelGGL(ms_merge_pass_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n, L,
-                               mo, split);
+                               mo, split, so);
         }
         CME_TRY(hipGetLastError());
         ki = ko;

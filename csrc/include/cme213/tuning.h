@@ -44,6 +44,7 @@ enum TuneKey : int {
     kTuneMergePart,        // CME_MERGE_PART: merge sort partitions: 4 / 8 / 16 / 32 / 64 lanes per tile in one search launch per pass (other positive: 64), 0 in-block searches, -1 auto (8 from 8M keys)
     kTuneMergeTile,        // CME_MERGE_TILE: merge sort output tile per merge-pass block, 4096 or 8192 keys (8192 with partitions)
     kTuneMergeBlock,       // CME_MERGE_BLOCK: merge sort block-sort tile, 8192 (512 lanes) or 16384 keys (1024 lanes); 0 auto (16384 for keys only from 4M)
+    kTuneMergeSamples,     // CME_MERGE_SAMPLES: merge sort run samples narrowing each partition search (1 on, 0 off)
     kTuneCount
 };
 

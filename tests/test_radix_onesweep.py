@@ -172,17 +172,20 @@ def test_merge_sort_skewed_and_stable(gpu, kind):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("part,tile", [(-1, 4096), (0, 4096), (4, 4096), (8, 4096), (16, 4096), (64, 4096), (8, 8192), (64, 8192)])
-def test_merge_sort_partition_arms(gpu, part, tile):
+@pytest.mark.parametrize("part,tile,samples", [(-1, 4096, 1), (0, 4096, 1), (4, 4096, 1), (8, 4096, 1), (8, 4096, 0),
+                                                (16, 4096, 1), (64, 4096, 1), (8, 8192, 1), (8, 8192, 0),
+                                                (64, 8192, 1)])
+def test_merge_sort_partition_arms(gpu, part, tile, samples):
     """Every way a merge pass finds its tile splits (tuning knob merge_part:
     G = 4 / 8 / 16 / 64 lanes per tile in one partition launch per pass; 0 each
-    block's cooperative search; -1 the size rule) and both merge tiles (merge_tile) sort keys
-    and key-value pairs stably, across pair ends, a last run without a
-    partner and passes of several search rounds."""
+    block's cooperative search; -1 the size rule), with and without the run
+    samples that narrow the search to one tile first (merge_samples), and both
+    merge tiles (merge_tile) sort keys and key-value pairs stably, across pair
+    ends, a last run without a partner and passes of several search rounds."""
     from cme213x.utils import tuning
 
     g = torch.Generator(device="cuda").manual_seed(9)
-    with tuning.override(merge_part=part, merge_tile=tile):
+    with tuning.override(merge_part=part, merge_tile=tile, merge_samples=samples):
         for n in (8193, 3 * 8192 + 4095, 1 << 20, 9 * (1 << 20) + 5):
             k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
             k[n // 2:] = k[n // 2:] % 11  # long runs of equal keys: ties across the split diagonals
