@@ -103,7 +103,9 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
     block sorts, then one LDS-staged merge-path pass per doubling of the run
     length; from 8M keys each pass first finds every tile's merge-path split
     in one launch (tuning knob merge_part), below that each merge block
-    searches its own; key transforms fused into the first and last kernels."""
+    searches its own; key transforms fused into the first and last kernels.
+    Tuning knob merge_way=4 merges four runs per pass instead (built and
+    measured slower on MI355X: profiles/sort_r6.md)."""
     if keys.dtype not in _MODES:
         raise TypeError(f"unsupported key dtype {keys.dtype}")
     k = keys.contiguous()
@@ -115,7 +117,7 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
         v = values.contiguous()
         vout, vtmp = torch.empty_like(v), torch.empty_like(v)
         vp, vo, vt = v.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
-    ws = _workspace(keys.device, (k.numel() + 4095) // 4096 * 16 + 256)  # = cme_merge_ws_bytes
+    ws = _workspace(keys.device, (k.numel() + 4095) // 4096 * 48 + 256)  # = cme_merge_ws_bytes
     _ext.call_hip("cme_merge_sort_ws", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
                   _MODES[keys.dtype], ws.data_ptr(), _ext.stream_ptr(keys.device))
     return (out, vout) if values is not None else out

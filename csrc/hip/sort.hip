@@ -494,6 +494,43 @@ __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* s
     }
 }
 
+// Stage 1 of a 4-way tile (ms_merge4_pass_kernel): the tile's slices of runs
+// A, B, C, D sit in LDS as X = [A | C] (C from index xa on) and Y = [B | D]
+// (D from y0 + yb on). Ordered by (pair, key) -- A and B pair 0, C and D
+// pair 1 -- X and Y are each sorted, and one merge path over them yields
+// [merge(A, B) | merge(C, D)], both stable (X first on ties). The pair bit
+// rides above the 32-bit key, so the exhausted-run sentinel ~0 sorts after
+// every real key and the step needs no bounds test. Same cursor discipline
+// as ms_merge16.
+__device__ __forceinline__ uint64_t ms_pair_key(const uint32_t* sk, int p, int e, int p1) {
+    const uint32_t x = sk[lp(p)];
+    return p < e ? ((uint64_t)(p >= p1 ? 1u : 0u) << 32) | x : ~0ull;
+}
+
+template <bool HAS_VALUES, int CAP>
+__device__ __forceinline__ void ms_merge16_pairs(const uint32_t* sk, const uint32_t* sv, int lx, int xa, int y0, int ly,
+                                                 int yb, int i, int j, uint32_t (&k)[kMsItems],
+                                                 uint32_t (&v)[kMsItems]) {
+    int pa = i, pb = y0 + j;
+    const int ea = lx, eb = y0 + ly, sa = xa, sb = y0 + yb;
+    uint64_t ka = ms_pair_key(sk, pa, ea, sa), kb = ms_pair_key(sk, pb, eb, sb);
+#pragma unroll
+    for (int q = 0; q < kMsItems; ++q) {
+        const bool take_a = ka <= kb;
+        k[q] = (uint32_t)(take_a ? ka : kb);
+        if constexpr (HAS_VALUES) {
+            const int x = take_a ? pa : pb;
+            v[q] = sv[lp(x < CAP ? x : CAP - 1)];
+        }
+        pa += take_a ? 1 : 0;
+        pb += take_a ? 0 : 1;
+        const int np = take_a ? pa : pb;  // one LDS load per step
+        const uint64_t nv = ms_pair_key(sk, np, take_a ? ea : eb, take_a ? sa : sb);
+        ka = take_a ? nv : ka;
+        kb = take_a ? kb : nv;
+    }
+}
+
 // Run samples of a pass's output for the next pass's partition search: the
 // first and the last key (uint32 codes) of every `st`-key tile of the array.
 struct MsSamples {
@@ -645,7 +682,9 @@ __global__ __launch_bounds__(256) void ms_partition_kernel(const uint32_t* __res
                                                            long long tile, long long ntiles,
                                                            long long* __restrict__ split,
                                                            const uint32_t* __restrict__ sfirst,
-                                                           const uint32_t* __restrict__ slast) {
+                                                           const uint32_t* __restrict__ slast,
+                                                           uint32_t* __restrict__ vfirst,
+                                                           uint32_t* __restrict__ vlast) {
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "partition group: 4-64 lanes");
     const long long t = ((long long)blockIdx.x * 256 + threadIdx.x) / G;
     const int sub = threadIdx.x % G;
@@ -696,7 +735,143 @@ __global__ __launch_bounds__(256) void ms_partition_kernel(const uint32_t* __res
             lo = nlo;
         }
     }
-    if (valid && sub == 0) split[t] = lo;
+    if (valid && sub == 0) {
+        split[t] = lo;
+        if (vfirst) {  // kernel-uniform: samples of the merged pair this pass would write (4-way passes)
+            const long long jb = diag - lo;
+            if (diag < la + lb) {
+                const bool ta = lo < la && (jb >= lb || A[lo] <= B[jb]);
+                vfirst[t] = ta ? A[lo] : B[jb];
+            }
+            if (diag > 0) {  // the key before this tile's first ends the previous tile
+                uint32_t e = lo > 0 ? A[lo - 1] : 0u;
+                if (jb > 0) e = max(e, B[jb - 1]);
+                vlast[t - 1] = e;
+            }
+            if (o0 + tile >= a0 + la + lb) vlast[t] = lb > 0 ? max(A[la - 1], B[lb - 1]) : A[la - 1];
+        }
+    }
+}
+
+// Exact 4-way splits of every output tile boundary of a 4-way pass (runs of
+// L merged four at a time into runs of 4L; one wave per boundary). The tile's
+// output is merge(AB, CD) with AB = merge(A, B) and CD = merge(C, D), neither
+// materialised. Per boundary at diagonal d of its group this finds
+//   x  = the AB keys among the first d outputs (outer merge path of AB / CD),
+//   sA = the A keys among the first x keys of AB, sC = the C keys among the
+//        first d - x keys of CD,
+// and writes (x, sA, sC) to b4[3 t ..]. Inputs from the launch before
+// (ms_partition_kernel at run length L with vfirst / vlast):
+//   split2 -- the A / B (C / D) split at every tile multiple of each pair, so
+//             any AB[m] lies in a window of one tile: the split of diagonal m
+//             is bracketed by split2 at the tile multiples around m;
+//   vfirst / vlast -- first / last key of every tile of AB and CD, which
+//             narrow the outer search to one tile's width first, as the run
+//             samples do for a 2-way pass.
+// Then 8 outer candidates x 8 lanes: each outer round evaluates AB[m] and
+// CD[d - 1 - m] for 8 candidates m by 8-ary inner searches in their
+// one-tile windows (two searches per lane group, loads in flight together).
+__global__ __launch_bounds__(256) void ms_partition4_kernel(const uint32_t* __restrict__ ki, long long n, long long L,
+                                                            long long tile, long long ntiles,
+                                                            const long long* __restrict__ split2,
+                                                            const uint32_t* __restrict__ vfirst,
+                                                            const uint32_t* __restrict__ vlast,
+                                                            long long* __restrict__ b4) {
+    const long long t = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;  // wave-uniform: one wave per boundary, no barriers
+    const int lane = lane_id(), c = lane >> 3, s = lane & 7;
+    const long long o0 = t * tile, g0 = o0 & ~(4 * L - 1), d = o0 - g0;
+    auto run = [&](long long off) { return off <= 0 ? 0ll : (off < L ? off : L); };
+    const long long la = run(n - g0), lb = run(n - g0 - L), lc = run(n - g0 - 2 * L), ld = run(n - g0 - 3 * L);
+    const long long lab = la + lb, lcd = lc + ld;
+    const uint32_t* A = ki + g0;
+    const uint32_t* B = A + la;
+    const uint32_t* C = ki + g0 + lab;
+    const uint32_t* D = C + lc;
+    const long long pab = g0 / tile, pcd = (g0 + lab) / tile;  // first tile of each pair (lab % tile == 0 if lcd > 0)
+    // the merge-path range of diagonal m in a pair, narrowed by split2
+    auto bounds = [&](long long m, long long lx, long long ly, long long p, long long& lo, long long& hi) {
+        lo = m - ly > 0 ? m - ly : 0;
+        hi = m < lx ? m : lx;
+        if (m > 0) {
+            const long long j = (m + tile - 1) / tile;  // m in ((j - 1) tile, j tile]
+            const long long slo = split2[p + j - 1];
+            const long long shi = j * tile >= lx + ly ? lx : split2[p + j];
+            lo = slo > lo ? slo : lo;
+            hi = shi < hi ? shi : hi;
+        }
+    };
+    const int gsh = lane & ~7;
+    // two 8-ary merge-path searches per lane group at once: (A, B) at m1, (C, D) at m2
+    auto search2 = [&](long long m1, long long& lo1, long long& hi1, long long m2, long long& lo2, long long& hi2) {
+        while (__ballot(lo1 < hi1 || lo2 < hi2)) {
+            const long long st1 = (hi1 - lo1 + 7) / 8, st2 = (hi2 - lo2 + 7) / 8;
+            const long long q1 = lo1 + s * st1, q2 = lo2 + s * st2;
+            const bool p1 = lo1 < hi1 && q1 < hi1 && A[q1] <= B[m1 - 1 - q1];
+            const bool p2 = lo2 < hi2 && q2 < hi2 && C[q2] <= D[m2 - 1 - q2];
+            const uint64_t f1m = (__ballot(!p1) >> gsh) & 0xffull, f2m = (__ballot(!p2) >> gsh) & 0xffull;
+            const int f1 = f1m ? __builtin_ctzll(f1m) : 8, f2 = f2m ? __builtin_ctzll(f2m) : 8;
+            if (lo1 < hi1) {
+                const long long nlo = f1 == 0 ? lo1 : lo1 + (long long)(f1 - 1) * st1 + 1, mf = lo1 + f1 * st1;
+                hi1 = f1 == 8 ? hi1 : (mf < hi1 ? mf : hi1);
+                lo1 = nlo;
+            }
+            if (lo2 < hi2) {
+                const long long nlo = f2 == 0 ? lo2 : lo2 + (long long)(f2 - 1) * st2 + 1, mf = lo2 + f2 * st2;
+                hi2 = f2 == 8 ? hi2 : (mf < hi2 ? mf : hi2);
+                lo2 = nlo;
+            }
+        }
+    };
+    long long lo = d - lcd > 0 ? d - lcd : 0, hi = d < lab ? d : lab;
+    if (lo < hi) {  // wave-uniform; narrow x to one tile of AB on the samples: Q(j tile) over 64 candidates
+        const long long j0 = (lo + tile - 1) / tile, j1 = (hi + tile - 1) / tile;
+        long long jlo = j0, jhi = j1;
+        const long long gb = (g0 + lab + d) / tile - 1;  // CD[d - 1 - j tile] ends tile gb - j
+        while (jlo < jhi) {
+            const long long st = (jhi - jlo + 63) / 64, j = jlo + lane * st;
+            const bool q = j < jhi && vfirst[pab + j] <= vlast[gb - j];
+            const uint64_t fails = __ballot(!q);
+            const int f = fails ? __builtin_ctzll(fails) : 64;
+            const long long nlo = f == 0 ? jlo : jlo + (long long)(f - 1) * st + 1, jf = jlo + f * st;
+            jhi = f == 64 ? jhi : (jf < jhi ? jf : jhi);
+            jlo = nlo;
+        }
+        if (jlo < j1 && jlo * tile < hi) hi = jlo * tile;
+        if (jlo > j0 && (jlo - 1) * tile + 1 > lo) lo = (jlo - 1) * tile + 1;
+    }
+    while (lo < hi) {  // wave-uniform outer search: Q(m) = AB[m] <= CD[d - 1 - m]
+        const long long st = (hi - lo + 7) / 8, m = lo + c * st;
+        const bool act = m < hi;
+        long long lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0;
+        if (act) {
+            bounds(m, la, lb, pab, lo1, hi1);
+            bounds(d - 1 - m, lc, ld, pcd, lo2, hi2);
+        }
+        search2(m, lo1, hi1, d - 1 - m, lo2, hi2);
+        bool q = false;
+        if (act) {  // AB[m] and CD[d - 1 - m] from their splits (X first on ties)
+            const long long m2 = d - 1 - m, jb = m - lo1, jd = m2 - lo2;
+            const uint32_t ab = lo1 < la && (jb >= lb || A[lo1] <= B[jb]) ? A[lo1] : B[jb];
+            const uint32_t cd = lo2 < lc && (jd >= ld || C[lo2] <= D[jd]) ? C[lo2] : D[jd];
+            q = ab <= cd;
+        }
+        const uint64_t fails = __ballot(!q);  // the 8 lanes of a candidate agree
+        const int f = fails ? __builtin_ctzll(fails) >> 3 : 8;
+        const long long nlo = f == 0 ? lo : lo + (long long)(f - 1) * st + 1, mf = lo + f * st;
+        hi = f == 8 ? hi : (mf < hi ? mf : hi);
+        lo = nlo;
+    }
+    const long long x = lo;
+    long long lo1, hi1, lo2, hi2;
+    bounds(x, la, lb, pab, lo1, hi1);
+    bounds(d - x, lc, ld, pcd, lo2, hi2);
+    search2(x, lo1, hi1, d - x, lo2, hi2);
+    if (lane == 0) {
+        b4[3 * t] = x;
+        b4[3 * t + 1] = lo1;
+        b4[3 * t + 2] = lo2;
+    }
 }
 
 // split: the pass's partitions from ms_partition_kernel, or nullptr for the
@@ -755,6 +930,73 @@ __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __res
     const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int x) { return sk[lp(na + x)]; }, na, nb, diag_l);
     uint32_t k[kMsItems], v[kMsItems];
     ms_merge16<HAS_VALUES, TILE>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
+    ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out, smp);
+}
+
+// One output tile of a 4-way pass (runs of L -> 4L): half the HBM passes of
+// the 2-way form for two LDS merge stages per tile. b4 holds every
+// boundary's (x, sA, sC) from ms_partition4_kernel, so the block loads
+// exactly its 4096 keys: the slices of A, B, C and D, laid out as X = [A | C],
+// Y = [B | D]. Stage 1 merges X and Y on (pair, key) into
+// [merge(A, B) | merge(C, D)] (ms_merge16_pairs); stage 2 merges those two.
+template <bool HAS_VALUES>
+__global__ __launch_bounds__(kMsThreads) void ms_merge4_pass_kernel(const uint32_t* __restrict__ ki,
+                                                                    uint32_t* __restrict__ ko,
+                                                                    const uint32_t* __restrict__ vi,
+                                                                    uint32_t* __restrict__ vo, long long n, long long L,
+                                                                    int mode_out, const long long* __restrict__ b4,
+                                                                    MsSamples smp) {
+    constexpr int NT = kMsThreads, TILE = kMsTile;
+    __shared__ uint32_t sk[lp_size(TILE) + 1];
+    __shared__ uint32_t sv[HAS_VALUES ? lp_size(TILE) : 1];
+    const int t = threadIdx.x;
+    const long long tile = xcd_remap(blockIdx.x, gridDim.x);
+    const long long o0 = tile * TILE;
+    const long long o1 = o0 + TILE < n ? o0 + TILE : n;
+    const long long g0 = o0 & ~(4 * L - 1);
+    auto run = [&](long long off) { return off <= 0 ? 0ll : (off < L ? off : L); };
+    const long long la = run(n - g0), lb = run(n - g0 - L), lc = run(n - g0 - 2 * L), ld = run(n - g0 - 3 * L);
+    const long long lab = la + lb, lcd = lc + ld;
+    const long long d0 = o0 - g0, d1 = o1 - g0;
+    const long long x0 = b4[3 * tile], a0 = b4[3 * tile + 1], c0 = b4[3 * tile + 2];
+    long long x1 = lab, a1 = la, c1 = lc;  // a tile ending its group takes the rest of all four runs
+    if (d1 != lab + lcd) {
+        x1 = b4[3 * tile + 3];
+        a1 = b4[3 * tile + 4];
+        c1 = b4[3 * tile + 5];
+    }
+    const long long bb0 = x0 - a0, bb1 = x1 - a1, dd0 = (d0 - x0) - c0, dd1 = (d1 - x1) - c1;
+    int na = (int)(a1 - a0), nb = (int)(bb1 - bb0), nc = (int)(c1 - c0), nd = (int)(dd1 - dd0);
+    if (na < 0 || nb < 0 || nc < 0 || nd < 0 || na + nb + nc + nd != d1 - d0 || a0 < 0 || bb0 < 0 || c0 < 0 ||
+        dd0 < 0 || a1 > la || bb1 > lb || c1 > lc || dd1 > ld)
+        na = nb = nc = nd = 0;  // never out of range
+    const long long ga = g0 + a0, gb = g0 + la + bb0, gc = g0 + lab + c0, gd = g0 + lab + lc + dd0;
+    const int nx = na + nc, cnt = nx + nb + nd;
+    for (int x = t; x < cnt; x += NT) {
+        const long long g = x < na ? ga + x : (x < nx ? gc + (x - na) : (x < nx + nb ? gb + (x - nx) : gd + (x - nx - nb)));
+        sk[lp(x)] = ki[g];
+        if constexpr (HAS_VALUES) sv[lp(x)] = vi[g];
+    }
+    __syncthreads();
+    const int p0 = kMsItems * t < cnt ? kMsItems * t : cnt;
+    uint32_t k[kMsItems], v[kMsItems];
+    {  // stage 1
+        const int i = ms_split([&](int x) { return ((uint64_t)(x >= na ? 1u : 0u) << 32) | sk[lp(x)]; },
+                               [&](int y) { return ((uint64_t)(y >= nb ? 1u : 0u) << 32) | sk[lp(nx + y)]; }, nx,
+                               nb + nd, p0);
+        ms_merge16_pairs<HAS_VALUES, TILE>(sk, sv, nx, na, nx, nb + nd, nb, i, p0 - i, k, v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kMsItems; ++q) {
+        sk[lp(kMsItems * t + q)] = k[q];
+        if constexpr (HAS_VALUES) sv[lp(kMsItems * t + q)] = v[q];
+    }
+    __syncthreads();
+    const int nab = na + nb;  // stage 2: merge(A, B) = [0, nab) with merge(C, D) = [nab, cnt)
+    const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int y) { return sk[lp(nab + y)]; }, nab, cnt - nab,
+                           p0);
+    ms_merge16<HAS_VALUES, TILE>(sk, sv, 0, nab, nab, cnt - nab, i, p0 - i, k, v);
     ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out, smp);
 }
 
@@ -962,7 +1204,7 @@ CME_EXPORT int cme_radix_sort_u32(uint32_t* keys, uint32_t* keys_alt, uint32_t* 
 // Stable merge sort of n keys from `in` into `out` (ping-pong through `tmp`;
 // `in` may equal `out`; values optional, likewise). mode: 0 uint32, 1 int32,
 // 2 float32 keys.
-CME_EXPORT long long cme_merge_ws_bytes(long long n) { return (long long)cdiv(n, kMsTile) * 16 + 256; }
+CME_EXPORT long long cme_merge_ws_bytes(long long n) { return (long long)cdiv(n, kMsTile) * 48 + 256; }
 
 // merge-pass output tile (tuning knob merge_tile: 4096 or 8192 keys; 8192
 // needs the partition launch)
@@ -974,7 +1216,9 @@ static int merge_tile(bool part) {
 // first computes all tile partitions in one launch (ms_partition_kernel);
 // without it each merge block searches its own (ms_coop_split). Layout:
 // split[tiles] (8 B), then the run samples first[tiles] and last[tiles]
-// (4 B each) that every kernel but the last writes for the next partition.
+// (4 B each) that every kernel but the last writes for the next partition,
+// then the 4-way passes' pair samples vfirst[tiles] / vlast[tiles] (4 B each)
+// and boundary splits b4[3 tiles] (8 B each).
 CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_t* vin,
                                  uint32_t* vout, uint32_t* vtmp, long long n, int mode, void* ws, void* stream) {
     hipStream_t s = as_stream(stream);
@@ -989,11 +1233,6 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     const long mb = cme::tune_get(cme::kTuneMergeBlock);
     const bool big = mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
     const long long btile = big ? 2 * kBsTile : kBsTile;
-    int npass = 0;
-    for (long long L = btile; L < n; L <<= 1) ++npass;
-    // the block sort writes where an even number of passes later lands in out
-    uint32_t* d0 = (npass & 1) ? tmp : out;
-    uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
     // partitions: tuning knob merge_part (G lanes per tile, 0 = in-block
     // searches, -1 = auto: G = 8 from 8M keys). Measured (profiles/sort_r5.md):
     // 48M int32 2.21 -> 1.59 ms, 16M 0.65 -> 0.55; at 1M and 4M the extra
@@ -1002,6 +1241,16 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     long part = ws ? cme::tune_get(cme::kTuneMergePart) : 0;
     if (part < 0) part = n >= (8ll << 20) ? 8 : 0;
     const int mtile = merge_tile(part != 0);
+    // 4-way passes (knob merge_way = 4, with partition launches and 4096-key
+    // tiles): runs of L -> 4L while at least three runs remain, a last 2-way
+    // pass for an odd number of doublings
+    const bool four = part != 0 && mtile == kMsTile && cme::tune_get(cme::kTuneMergeWay) == 4;
+    auto next_len = [&](long long L) { return four && 2 * L < n ? 4 * L : 2 * L; };
+    int npass = 0;
+    for (long long L = btile; L < n; L = next_len(L)) ++npass;
+    // the block sort writes where an even number of passes later lands in out
+    uint32_t* d0 = (npass & 1) ? tmp : out;
+    uint32_t* v0 = vin ? ((npass & 1) ? vtmp : vout) : nullptr;
     const unsigned btiles = cdiv(n, btile), tiles = cdiv(n, mtile);
     const int m0 = npass ? 0 : mode;
     // run samples (knob merge_samples, default on): written by every kernel
@@ -1012,6 +1261,15 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     if (samples) {
         uint32_t* sbase = (uint32_t*)((char*)ws + (size_t)cdiv(n, kMsTile) * 8);
         smp = MsSamples{sbase, sbase + cdiv(n, kMsTile), mtile};
+    }
+    uint32_t* vfirst = nullptr;
+    uint32_t* vlast = nullptr;
+    long long* b4 = nullptr;
+    if (four) {
+        const size_t nt = cdiv(n, kMsTile);
+        vfirst = (uint32_t*)((char*)ws + nt * 16);
+        vlast = vfirst + nt;
+        b4 = (long long*)((char*)ws + nt * 24);
     }
     const MsSamples smp0 = npass ? smp : none;
     if (big && vin)
@@ -1029,17 +1287,20 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     CME_TRY(hipGetLastError());
     const uint32_t *ki = d0, *vi = v0;
     int p = 0;
-    for (long long L = btile; L < n; L <<= 1, ++p) {
+    for (long long L = btile; L < n; L = next_len(L), ++p) {
         const bool last = p == npass - 1;
+        const bool w4 = four && 2 * L < n;
         uint32_t* ko = (ki == out) ? tmp : out;
         uint32_t* vo = vin ? ((vi == vout) ? vtmp : vout) : nullptr;
         long long* split = part ? (long long*)ws : nullptr;
+        uint32_t* pf = w4 ? vfirst : nullptr;
+        uint32_t* pl = w4 ? vlast : nullptr;
         if (split) {
             const int g = part == 4 || part == 8 || part == 16 || part == 32 ? (int)part : 64;
             const dim3 grid(cdiv((long long)tiles * g, 256));
 #define CME_PART(G)                                                                                               \
     hipLaunchKernelGGL(ms_partition_kernel<G>, grid, dim3(256), 0, s, ki, n, L, (long long)mtile, (long long)tiles, \
-                       split, smp.first, smp.last)
+                       split, smp.first, smp.last, pf, pl)
             if (g == 4) CME_PART(4);
             else if (g == 8) CME_PART(8);
             else if (g == 16) CME_PART(16);
@@ -1049,7 +1310,16 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
         }
         const int mo = last ? mode : 0;
         const MsSamples so = last ? none : smp;
-        if (mtile == 8192) {
+        if (w4) {
+            hipLaunchKernelGGL(ms_partition4_kernel, dim3(cdiv((long long)tiles, 4)), dim3(256), 0, s, ki, n, L,
+                               (long long)mtile, (long long)tiles, split, vfirst, vlast, b4);
+            if (vin)
+                hipLaunchKernelGGL(ms_merge4_pass_kernel<true>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo, n,
+                                   L, mo, b4, so);
+            else
+                hipLaunchKernelGGL(ms_merge4_pass_kernel<false>, dim3(tiles), dim3(kMsThreads), 0, s, ki, ko, vi, vo,
+                                   n, L, mo, b4, so);
+        } else if (mtile == 8192) {
             if (vin)
                 hipLaunchKernelGGL((ms_merge_pass_kernel<true, 512>), dim3(tiles), dim3(512), 0, s, ki, ko, vi, vo, n,
                                    L, mo, split, so);
@@ -1086,3 +1356,5 @@ CME_REGISTER_KERNEL(radix_upsweep, 256, radix_upsweep_kernel<4>);
 CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
 CME_REGISTER_KERNEL(ms_block_sort, 512, ms_block_sort_kernel<false>);
 CME_REGISTER_KERNEL(ms_merge_pass, 256, ms_merge_pass_kernel<false>);
+CME_REGISTER_KERNEL(ms_merge4_pass, 256, ms_merge4_pass_kernel<false>);
+CME_REGISTER_KERNEL(ms_partition4, 256, ms_partition4_kernel);

@@ -198,6 +198,41 @@ def test_merge_sort_partition_arms(gpu, part, tile, samples):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("way,part,samples,block", [(4, 8, 1, 0), (4, 8, 0, 8192), (4, 64, 1, 16384), (4, 4, 1, 8192),
+                                                    (2, 8, 1, 0)])
+def test_merge_sort_four_way_passes(gpu, way, part, samples, block):
+    """4-way merge passes (tuning knob merge_way; csrc/hip/sort.hip
+    ms_partition4_kernel + ms_merge4_pass_kernel) sort keys and key-value
+    pairs stably: groups of four runs, three (D empty), two and one at the
+    array's end, an odd number of doublings (a last 2-way pass), ties across
+    every run boundary, and all-equal / presorted / reversed inputs."""
+    from cme213x.utils import tuning
+
+    g = torch.Generator(device="cuda").manual_seed(21)
+    sizes = (8193, 3 * 8192 + 5, 5 * 8192, 16 * 8192 + 4095, 17 * 16384 + 1, 3 * (1 << 20) + 77, 9 * (1 << 20) + 5)
+    with tuning.override(merge_way=way, merge_part=part, merge_samples=samples, merge_block=block):
+        for n in sizes:
+            k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+            k[n // 2:] = k[n // 2:] % 13  # long runs of equal keys
+            v = torch.arange(n, device="cuda", dtype=torch.int32)
+            ks, vs = sort(k, values=v, algo="merge")
+            rk, ri = torch.sort(k.cpu().long(), stable=True)
+            assert torch.equal(ks.cpu().long(), rk), n
+            assert torch.equal(vs.cpu().long(), ri), n
+            assert torch.equal(sort(k, algo="merge").cpu().long(), rk), n
+        n = 3 * (1 << 20) + 11
+        for kind in ("equal", "sorted", "reversed", "fewbits"):
+            k = _keys(n, torch.int32, kind).to(gpu)
+            v = torch.arange(n, device="cuda", dtype=torch.int32)
+            ks, vs = sort(k, values=v, algo="merge")
+            ref = torch.sort(k.cpu(), stable=True)
+            assert torch.equal(ks.cpu(), ref.values), kind
+            assert torch.equal(vs.cpu(), ref.indices.to(torch.int32)), kind
+        x = torch.randn(5 * (1 << 20) + 3, device="cuda", generator=g)
+        assert torch.equal(sort(x, algo="merge").cpu(), torch.sort(x.cpu()).values)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("block", [0, 8192, 16384])
 def test_merge_sort_block_tiles(gpu, block):
     """Both block-sort tiles (tuning knob merge_block: 512 or 1024 lanes, or
