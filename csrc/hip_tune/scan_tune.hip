@@ -87,3 +87,113 @@ CME_EXPORT int cme_spmv_scan_tune(float* a, const float* xx, const uint32_t* fla
 #undef SPT
     return (int)hipErrorInvalidValue;
 }
+
+// ---------------------------------------------------------------------------
+// Tuning arms of the Blelloch tile-parallel reduce-then-scan (f32, exclusive;
+// production: scan_kernels.h launch_tree_rts, BASELINE config #3).
+// benchmarks/tune_tree_scan.py times them cold.
+//   arm 0 production                    arm 1 K1 grid 2048
+//   arm 2 K1 two tiles in flight        arm 3 K1 one tile per block (grid = tiles)
+//   arm 4 K3 grid 2048                  arm 5 = 2 + 4
+//   arm 6 K2 fused into K1: the last K1 block to finish (one device-scope
+//         atomic per block) scans the tile sums, saving a launch
+//   arm 7 = 2 + 6
+// ws: 4 B per 4096-element tile, then a 256-B aligned counter word (arms 6-7;
+// it must start zeroed, the last block leaves it zeroed).
+namespace {
+template <int PF>
+__global__ __launch_bounds__(256) void tile_reduce_tune_kernel(const float* __restrict__ in, long long n, int ntiles,
+                                                               float* __restrict__ tsum, unsigned* __restrict__ counter) {
+    __shared__ float lds[4];
+    __shared__ unsigned s_last;
+    Vec4<float> q[PF][4];
+    const int G = (int)gridDim.x;
+    int tile = blockIdx.x;
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+        if (tile + p * G < ntiles) tile_load4(in, (long long)(tile + p * G) * kTreeTile, n, q[p]);
+    for (; tile < ntiles; tile += G) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = acc + ((q[0][k].x + q[0][k].y) + (q[0][k].z + q[0][k].w));
+#pragma unroll
+        for (int p = 0; p + 1 < PF; ++p)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[p][k] = q[p + 1][k];
+        if (tile + PF * G < ntiles) tile_load4(in, (long long)(tile + PF * G) * kTreeTile, n, q[PF - 1]);
+        const float r = block_reduce<4>(acc, lds, OpAdd());
+        if (threadIdx.x == 0) tsum[tile] = r;
+    }
+    if (!counter) return;  // block-uniform
+    __threadfence();       // this block's tile sums, device-wide, before its arrival
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(counter, 1u) == (unsigned)G - 1u ? 1u : 0u;
+    lds_bcast_sync();
+    if (!s_last) return;
+    __threadfence();  // every other block's tile sums
+    // exclusive scan of the ntiles sums in place: 16 per thread per round
+    constexpr int kPer = 16, kRound = 256 * kPer;
+    __shared__ float stage[tpad(kRound)];
+    __shared__ float wl[4];
+    const int t = threadIdx.x;
+    float carry = 0.f;
+    for (int base = 0; base < ntiles; base += kRound) {
+#pragma unroll
+        for (int k = 0; k < kPer / 4; ++k) {
+            const int e = (k * 256 + t) * 4;
+            const Vec4<float> v = load_v4(tsum, (long long)base + e, ntiles, 0.f);
+            stage[tpad(e)] = v.x;
+            stage[tpad(e + 1)] = v.y;
+            stage[tpad(e + 2)] = v.z;
+            stage[tpad(e + 3)] = v.w;
+        }
+        __syncthreads();
+        float v[kPer], acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            v[k] = stage[tpad(t * kPer + k)];
+            acc = acc + v[k];
+        }
+        float tot;
+        float run = carry + block_exclusive_scan<4>(acc, wl, tot, OpAdd());
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            stage[tpad(t * kPer + k)] = run;
+            run = run + v[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer / 4; ++k) {
+            const int e = (k * 256 + t) * 4;
+            store_v4(tsum, (long long)base + e, ntiles,
+                     Vec4<float>{stage[tpad(e)], stage[tpad(e + 1)], stage[tpad(e + 2)], stage[tpad(e + 3)]});
+        }
+        __syncthreads();
+        carry = carry + tot;
+    }
+    if (t == 0) *counter = 0u;  // ready for the next call on this workspace
+}
+}  // namespace
+
+CME_EXPORT int cme_scan_tree_tune(const float* in, float* out, long long n, int arm, void* ws, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (n <= 0) return 0;
+    const long long tiles = (n + kTreeTile - 1) / kTreeTile;
+    if (tiles >= (1ll << 31)) return (int)hipErrorInvalidValue;
+    const int nt = (int)tiles;
+    if (arm == 0) return launch_tree_rts<float>(in, out, n, 0, 1, ws, s);
+    float* part = (float*)ws;
+    unsigned* counter = (arm == 6 || arm == 7) ? (unsigned*)((char*)ws + ((size_t)nt * 4 + 255) / 256 * 256) : nullptr;
+    const int cap = [&] { int c = nt < kRtsBlocks ? nt : kRtsBlocks; return c; }();
+    int g1 = cap, g3 = cap;
+    if (arm == 1) g1 = nt < 2048 ? nt : 2048;
+    if (arm == 3) g1 = nt;
+    if (arm == 4 || arm == 5) g3 = nt < 2048 ? nt : 2048;
+    if (arm == 2 || arm == 5 || arm == 7)
+        hipLaunchKernelGGL(tile_reduce_tune_kernel<2>, dim3(g1), dim3(256), 0, s, in, n, nt, part, counter);
+    else
+        hipLaunchKernelGGL(tile_reduce_tune_kernel<1>, dim3(g1), dim3(256), 0, s, in, n, nt, part, counter);
+    if (!counter) hipLaunchKernelGGL(rts_partials_kernel<float>, dim3(1), dim3(1024), 0, s, part, nt);
+    hipLaunchKernelGGL((tile_tree_scan_kernel<float, true, 0>), dim3(g3), dim3(256), 0, s, in, out, n, nt, part);
+    CME_LAUNCH_STATUS();
+}
