@@ -461,6 +461,37 @@ __device__ __forceinline__ int ms_split(FA A, FB B, int la, int lb, int diag) {
     return lo;
 }
 
+// LDS word i of a padded buffer, the byte offset (i + i / 16) * 4 written out
+// so that it folds into one v_add_lshl_u32
+__device__ __forceinline__ uint32_t ldsw(const uint32_t* sk, int i) {
+    return *(const uint32_t*)((const char*)sk + ((unsigned)(i + (i >> 4)) << 2));
+}
+
+// The same split by binary lifting: halving steps from smax, a power of two
+// with 2 smax - 1 >= the search range (uniform across the block, so the loop
+// is scalar: no divergent trip counts, no exec bookkeeping). Step st tries to
+// move lo past st more candidates; a probe beyond the range counts as false
+// and reads a clamped in-range index. ~11 VALU per step against ~17 plus the
+// loop's exec masks for the bisection (profiles/sort_r6.md).
+__device__ __forceinline__ int ms_split_lift(const uint32_t* sk, int a0, int la, int b0, int lb, int diag, int smax) {
+    const int lo0 = diag - lb > 0 ? diag - lb : 0, hi0 = diag < la ? diag : la;
+    const int kb = b0 + diag - 1;
+    int lo = lo0;
+    for (int st = smax; st > 0; st >>= 1) {
+        const int m = lo + st - 1;
+        const int mc = max(min(m, hi0 - 1), 0);
+        const bool q = m < hi0 && ldsw(sk, a0 + mc) <= ldsw(sk, kb - mc);
+        lo = q ? m + 1 : lo;
+    }
+    return lo;
+}
+
+// the smax of ms_split_lift for runs of la and lb keys (block-uniform)
+__device__ __forceinline__ int ms_lift_top(int la, int lb) {
+    const int r = la < lb ? la : lb;  // a diagonal's candidates span at most min(la, lb) + 1
+    return __builtin_amdgcn_readfirstlane(r > 0 ? 1 << (31 - __builtin_clz(r)) : 0);
+}
+
 // sequential merge of kMsItems outputs from A = [a0, a0+la) / B = [b0, b0+lb)
 // (logical LDS indices, padded on access) into registers. Branch-free: every
 // step selects its output, advances one of the two cursors and loads that
@@ -475,6 +506,28 @@ __device__ __forceinline__ void ms_merge16(const uint32_t* sk, const uint32_t* s
     uint32_t ka = sk[lp(pa)], kb = sk[lp(pb)];
     ka = pa < ea ? ka : 0xffffffffu;
     kb = pb < eb ? kb : 0xffffffffu;
+    if constexpr (!HAS_VALUES) {
+        // Keys only: equal keys are indistinguishable, so the step takes
+        // min(ka, kb) and advances A on ka <= kb with no bounds test. An
+        // exhausted run reads as all-ones; if the other run's key is all-ones
+        // too, every remaining output is all-ones whichever cursor moves (a
+        // cursor past its end keeps reading all-ones through the guard). 12
+        // VALU per step instead of ~19 (profiles/sort_r6.md).
+#pragma unroll
+        for (int q = 0; q < kMsItems; ++q) {
+            const bool take_a = ka <= kb;
+            k[q] = min(ka, kb);
+            pa += take_a ? 1 : 0;
+            pb += take_a ? 0 : 1;
+            const int np = take_a ? pa : pb;
+            // byte offset (np + np / 16) * 4 written out, so it folds into one v_add_lshl_u32
+            uint32_t nv = *(const uint32_t*)((const char*)sk + ((unsigned)(np + (np >> 4)) << 2));
+            nv = np < (take_a ? ea : eb) ? nv : 0xffffffffu;
+            ka = take_a ? nv : ka;
+            kb = take_a ? kb : nv;
+        }
+        return;
+    }
 #pragma unroll
     for (int q = 0; q < kMsItems; ++q) {
         const bool take_a = pb >= eb || (pa < ea && ka <= kb);
@@ -630,6 +683,107 @@ __global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __res
         ms_merge16<HAS_VALUES, BTILE>(sk, sv, a0, L, b0, L, i, diag - i, k, v);
     }
     ms_store_tile<HAS_VALUES, BS>(sk, sv, k, v, ko, vo, base, cnt, mode_out, smp);
+}
+
+// Keys-only block sort by LSD radix in LDS (the base case of the merge sort,
+// as the hw4 merge sort hands blocks below its threshold to std::sort,
+// hw/hw4/programming/mergesort.cpp:80-84): a 1024-lane block sorts its
+// 16384-key tile with four 8-bit digit passes that never leave LDS. Per pass
+// every wave ranks its 1024 keys stably (items in (k, lane) order: one
+// returning LDS atomic per key, or the ballot match where the device fails the
+// lane-order check -- the radix downsweep's two ranking kinds), the 16 waves'
+// digit counts become per-(wave, digit) bases (column prefix + block scan of
+// the 256 digit totals), and the keys scatter to their digit positions. ~20
+// VALU per key and pass against ~28 per key and merge round for the merge
+// block sort's ten rounds (profiles/sort_r6.md). Padding keys of a partial
+// tile are all-ones and, stable, stay behind every real key. LDS: 64 KiB of
+// keys + 16 KiB of counts = 80 KiB and <= 64 VGPRs (8 waves per SIMD): two
+// blocks per CU.
+template <int RANK, int ITEMS = kMsItems>
+__global__ __launch_bounds__(1024, ITEMS == 16 ? 8 : 4) void ms_block_radix_kernel(const uint32_t* __restrict__ ki,
+                                                                  uint32_t* __restrict__ ko, long long n, int mode_in,
+                                                                  int mode_out, MsSamples smp) {
+    constexpr int NT = 1024, NW = NT / kWave, TILE = NT * ITEMS;
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_whist[NW][kBins];
+    uint32_t* s_tmp = s_keys;  // the block scan's wave totals (s_keys is idle between reload and scatter)
+    const int tid = threadIdx.x, lane = lane_id(), wid = tid / kWave;
+    const long long base = (long long)blockIdx.x * TILE;
+    const int cnt = (int)(n - base < TILE ? n - base : TILE);
+    uint32_t key[ITEMS], rank2[ITEMS / 2];  // in-wave ranks (< 1024), two per register
+    // wave-striped items: item k of lane l is key wid*1024 + k*64 + l (memory order (k, l))
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const int i = wid * (kWave * ITEMS) + k * kWave + lane;
+        key[k] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
+    }
+    auto put_rank = [&](int k, uint32_t r) {
+        rank2[k / 2] = (k & 1) ? (rank2[k / 2] | (r << 16)) : r;
+    };
+    for (int shift = 0; shift < 32; shift += kRadixBits) {
+#pragma unroll
+        for (int w = 0; w < NW * kBins / NT; ++w) (&s_whist[0][0])[w * NT + tid] = 0u;
+        __syncthreads();
+        if constexpr (RANK == kRankLanes) {
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                const uint32_t d = digit_of(key[k], shift);
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+                if (__ballot(d != d0) == 0) {  // one digit in the wave: one atomic
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(&s_whist[wid][d0], (uint32_t)kWave);
+                    put_rank(k, (uint32_t)__builtin_amdgcn_readfirstlane((int)b) + (uint32_t)lane);
+                } else {
+                    put_rank(k, atomicAdd(&s_whist[wid][d], 1u));  // same-address lanes resolve in lane order
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) {
+                const uint32_t d = digit_of(key[k], shift);
+                const uint64_t peers = match_digit(d, true);
+                const uint32_t below = (uint32_t)__builtin_popcountll(peers & ((1ull << lane) - 1ull));
+                const uint32_t prev = s_whist[wid][d];
+                put_rank(k, prev + below);
+                if (below == 0) s_whist[wid][d] = prev + (uint32_t)__builtin_popcountll(peers);
+                __builtin_amdgcn_sched_barrier(0);  // keep each item's ballots next to its LDS update
+            }
+        }
+        __syncthreads();
+        // per digit: exclusive prefix over the waves, then the block scan of the digit totals
+        uint32_t run = 0;
+        if (tid < kBins) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const uint32_t c = s_whist[w][tid];
+                s_whist[w][tid] = run;
+                run += c;
+            }
+        }
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan<NW>(tid < kBins ? run : 0u, s_tmp, tot, OpAdd());
+        if (tid < kBins) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) s_whist[w][tid] += ex;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) s_keys[s_whist[wid][digit_of(key[k], shift)] + ((rank2[k / 2] >> (16 * (k & 1))) & 0xffffu)] = key[k];
+        __syncthreads();
+        if (shift + kRadixBits < 32) {
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) key[k] = s_keys[wid * (kWave * ITEMS) + k * kWave + lane];
+        }
+    }
+    if (smp.first) {  // block-uniform: the next partition's run samples
+        const int nq = (cnt + smp.st - 1) / smp.st;
+        for (int q = tid; q < nq; q += NT) {
+            const int e = (q + 1) * smp.st < cnt ? (q + 1) * smp.st : cnt;
+            smp.first[base / smp.st + q] = s_keys[q * smp.st];
+            smp.last[base / smp.st + q] = s_keys[e - 1];
+        }
+    }
+    for (int i = tid; i < cnt; i += NT) ko[base + i] = ms_key_out(s_keys[i], mode_out);
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -927,7 +1081,7 @@ __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __res
     __syncthreads();
     const int cnt = na + nb;
     const int diag_l = kMsItems * t < cnt ? kMsItems * t : cnt;
-    const int i = ms_split([&](int x) { return sk[lp(x)]; }, [&](int x) { return sk[lp(na + x)]; }, na, nb, diag_l);
+    const int i = ms_split_lift(sk, 0, na, na, nb, diag_l, ms_lift_top(na, nb));
     uint32_t k[kMsItems], v[kMsItems];
     ms_merge16<HAS_VALUES, TILE>(sk, sv, 0, na, na, nb, i, diag_l - i, k, v);
     ms_store_tile<HAS_VALUES, NT>(sk, sv, k, v, ko, vo, o0, cnt, mode_out, smp);
@@ -1231,8 +1385,22 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     // 1M 0.099 -> 0.109 and key-value 48M 2.79 -> 2.90, where the 1024-lane
     // blocks halve the resident blocks per CU; profiles/sort_r5.md)
     const long mb = cme::tune_get(cme::kTuneMergeBlock);
-    const bool big = mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
-    const long long btile = big ? 2 * kBsTile : kBsTile;
+    // keys-only block sorts by LDS radix (knob merge_block_sort: 1 radix, 0
+    // the merge-network block sort) on a device that passed the lane-order
+    // check (the ballot-match ranks would spill at the VGPRs two blocks per CU
+    // allow: the merge block sort instead); they also take 32768-key tiles
+    // (merge_block=32768: 128 KiB of LDS, one block per CU, one merge pass
+    // fewer)
+    bool radix_block = false;
+    if (!vin && n > kBsTile && cme::tune_get(cme::kTuneMergeBlockSort) != 0) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+        radix_block = cme_radix_lane_order(capturing ? 0 : 1) != 0;
+    }
+    const bool huge = radix_block && mb == 32768;
+    const bool big = huge || mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
+    radix_block = radix_block && big;
+    const long long btile = huge ? 4 * kBsTile : (big ? 2 * kBsTile : kBsTile);
     // partitions: tuning knob merge_part (G lanes per tile, 0 = in-block
     // searches, -1 = auto: G = 8 from 8M keys). Measured (profiles/sort_r5.md):
     // 48M int32 2.21 -> 1.59 ms, 16M 0.65 -> 0.55; at 1M and 4M the extra
@@ -1272,7 +1440,13 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
         b4 = (long long*)((char*)ws + nt * 24);
     }
     const MsSamples smp0 = npass ? smp : none;
-    if (big && vin)
+    if (huge)
+        hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, 32>), dim3(btiles), dim3(1024), 0, s, in, d0, n, mode,
+                           m0, smp0);
+    else if (radix_block)
+        hipLaunchKernelGGL(ms_block_radix_kernel<kRankLanes>, dim3(btiles), dim3(1024), 0, s, in, d0, n, mode, m0,
+                           smp0);
+    else if (big && vin)
         hipLaunchKernelGGL((ms_block_sort_kernel<true, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s, in,
                            d0, vin, v0, n, mode, m0, smp0);
     else if (big)
@@ -1357,4 +1531,5 @@ CME_REGISTER_KERNEL(radix_downsweep_kv, 256, radix_downsweep_kernel<true>);
 CME_REGISTER_KERNEL(ms_block_sort, 512, ms_block_sort_kernel<false>);
 CME_REGISTER_KERNEL(ms_merge_pass, 256, ms_merge_pass_kernel<false>);
 CME_REGISTER_KERNEL(ms_merge4_pass, 256, ms_merge4_pass_kernel<false>);
+CME_REGISTER_KERNEL(ms_block_radix, 1024, ms_block_radix_kernel<kRankLanes>);
 CME_REGISTER_KERNEL(ms_partition4, 256, ms_partition4_kernel);

@@ -233,6 +233,40 @@ def test_merge_sort_four_way_passes(gpu, way, part, samples, block):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block_sort,block", [(0, 16384), (1, 16384), (1, 32768)])
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float32, torch.uint32])
+def test_merge_sort_radix_block_sort(gpu, block_sort, block, dtype):
+    """Keys-only merge sorts from 4M keys start from 16384-key block sorts:
+    the LDS radix block sort (tuning knob merge_block_sort=1, csrc/hip/sort.hip
+    ms_block_radix_kernel; also with 32768-key tiles) or the merge-network
+    one (0). Both give torch.sort's
+    keys for int32 / float32 (signed zeros, infinities) / uint32 codes, full
+    and partial tiles, one tile, and heavy duplicates."""
+    from cme213x.utils import tuning
+
+    g = torch.Generator(device="cuda").manual_seed(31)
+    with tuning.override(merge_block_sort=block_sort, merge_block=block):
+        for n in (1, 16383, 16384, 16385, 32768, 32769, 5 * 16384 + 77, 4 * (1 << 20) + 9, 9 * (1 << 20)):
+            if dtype == torch.float32:
+                k = torch.randn(n, device="cuda", generator=g)
+                k[: n // 5] = torch.round(k[: n // 5])  # duplicates and signed zeros
+                if n > 8:
+                    k[:4] = torch.tensor([float("inf"), float("-inf"), -0.0, 0.0], device="cuda")
+                ref = torch.sort(k.cpu()).values
+                out = sort(k, algo="merge").cpu()
+                assert torch.equal(out.view(torch.int32), ref.view(torch.int32)) or torch.equal(out, ref), n
+                continue
+            k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
+            k[n // 2:] = k[n // 2:] % 17
+            if dtype == torch.uint32:
+                ku = k.view(torch.uint32)
+                ref = torch.sort(ku.cpu().view(torch.int32).long() & 0xFFFFFFFF).values
+                assert torch.equal(sort(ku, algo="merge").cpu().view(torch.int32).long() & 0xFFFFFFFF, ref), n
+            else:
+                assert torch.equal(sort(k, algo="merge").cpu(), torch.sort(k.cpu()).values), n
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("block", [0, 8192, 16384])
 def test_merge_sort_block_tiles(gpu, block):
     """Both block-sort tiles (tuning knob merge_block: 512 or 1024 lanes, or
