@@ -699,23 +699,25 @@ __global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __res
 // tile are all-ones and, stable, stay behind every real key. LDS: 64 KiB of
 // keys + 16 KiB of counts = 80 KiB and <= 64 VGPRs (8 waves per SIMD): two
 // blocks per CU.
-template <int RANK, int ITEMS = kMsItems>
-__global__ __launch_bounds__(1024, ITEMS == 16 ? 8 : 4) void ms_block_radix_kernel(const uint32_t* __restrict__ ki,
-                                                                  uint32_t* __restrict__ ko, long long n, int mode_in,
-                                                                  int mode_out, MsSamples smp) {
-    constexpr int NT = 1024, NW = NT / kWave, TILE = NT * ITEMS;
+template <int RANK, int ITEMS = kMsItems, bool HAS_VALUES = false, int NT = 1024>
+__global__ __launch_bounds__(NT, NT == 1024 ? (ITEMS == 16 ? 8 : 4) : 4) void ms_block_radix_kernel(
+    const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko, const uint32_t* __restrict__ vi,
+    uint32_t* __restrict__ vo, long long n, int mode_in, int mode_out, MsSamples smp) {
+    constexpr int NW = NT / kWave, TILE = NT * ITEMS;
     __shared__ uint32_t s_keys[TILE];
+    __shared__ uint32_t s_vals[HAS_VALUES ? TILE : 1];
     __shared__ uint32_t s_whist[NW][kBins];
     uint32_t* s_tmp = s_keys;  // the block scan's wave totals (s_keys is idle between reload and scatter)
     const int tid = threadIdx.x, lane = lane_id(), wid = tid / kWave;
     const long long base = (long long)blockIdx.x * TILE;
     const int cnt = (int)(n - base < TILE ? n - base : TILE);
-    uint32_t key[ITEMS], rank2[ITEMS / 2];  // in-wave ranks (< 1024), two per register
+    uint32_t key[ITEMS], val[HAS_VALUES ? ITEMS : 1], rank2[ITEMS / 2];  // in-wave ranks (< 1024), two per register
     // wave-striped items: item k of lane l is key wid*1024 + k*64 + l (memory order (k, l))
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         const int i = wid * (kWave * ITEMS) + k * kWave + lane;
         key[k] = i < cnt ? ms_key_in(ki[base + i], mode_in) : 0xffffffffu;
+        if constexpr (HAS_VALUES) val[k] = i < cnt ? vi[base + i] : 0u;
     }
     auto put_rank = [&](int k, uint32_t r) {
         rank2[k / 2] = (k & 1) ? (rank2[k / 2] | (r << 16)) : r;
@@ -768,11 +770,18 @@ __global__ __launch_bounds__(1024, ITEMS == 16 ? 8 : 4) void ms_block_radix_kern
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < ITEMS; ++k) s_keys[s_whist[wid][digit_of(key[k], shift)] + ((rank2[k / 2] >> (16 * (k & 1))) & 0xffffu)] = key[k];
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t pos = s_whist[wid][digit_of(key[k], shift)] + ((rank2[k / 2] >> (16 * (k & 1))) & 0xffffu);
+            s_keys[pos] = key[k];
+            if constexpr (HAS_VALUES) s_vals[pos] = val[k];
+        }
         __syncthreads();
         if (shift + kRadixBits < 32) {
 #pragma unroll
-            for (int k = 0; k < ITEMS; ++k) key[k] = s_keys[wid * (kWave * ITEMS) + k * kWave + lane];
+            for (int k = 0; k < ITEMS; ++k) {
+                key[k] = s_keys[wid * (kWave * ITEMS) + k * kWave + lane];
+                if constexpr (HAS_VALUES) val[k] = s_vals[wid * (kWave * ITEMS) + k * kWave + lane];
+            }
         }
     }
     if (smp.first) {  // block-uniform: the next partition's run samples
@@ -783,7 +792,10 @@ __global__ __launch_bounds__(1024, ITEMS == 16 ? 8 : 4) void ms_block_radix_kern
             smp.last[base / smp.st + q] = s_keys[e - 1];
         }
     }
-    for (int i = tid; i < cnt; i += NT) ko[base + i] = ms_key_out(s_keys[i], mode_out);
+    for (int i = tid; i < cnt; i += NT) {
+        ko[base + i] = ms_key_out(s_keys[i], mode_out);
+        if constexpr (HAS_VALUES) vo[base + i] = s_vals[i];
+    }
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -1392,14 +1404,16 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     // (merge_block=32768: 128 KiB of LDS, one block per CU, one merge pass
     // fewer)
     bool radix_block = false;
-    if (!vin && n > kBsTile && cme::tune_get(cme::kTuneMergeBlockSort) != 0) {
+    if (n > kBsTile && cme::tune_get(cme::kTuneMergeBlockSort) != 0) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
         radix_block = cme_radix_lane_order(capturing ? 0 : 1) != 0;
     }
-    const bool huge = radix_block && mb == 32768;
+    const bool huge = radix_block && !vin && mb == 32768;
     const bool big = huge || mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
-    radix_block = radix_block && big;
+    // key-value pairs: the radix block sort at 8192-key tiles (512 lanes)
+    const bool radix_kv = radix_block && vin && !big;
+    radix_block = radix_block && !vin && big;
     const long long btile = huge ? 4 * kBsTile : (big ? 2 * kBsTile : kBsTile);
     // partitions: tuning knob merge_part (G lanes per tile, 0 = in-block
     // searches, -1 = auto: G = 8 from 8M keys). Measured (profiles/sort_r5.md):
@@ -1441,11 +1455,14 @@ CME_EXPORT int cme_merge_sort_ws(const uint32_t* in, uint32_t* out, uint32_t* tm
     }
     const MsSamples smp0 = npass ? smp : none;
     if (huge)
-        hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, 32>), dim3(btiles), dim3(1024), 0, s, in, d0, n, mode,
-                           m0, smp0);
+        hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, 32>), dim3(btiles), dim3(1024), 0, s, in, d0, vin, v0,
+                           n, mode, m0, smp0);
     else if (radix_block)
-        hipLaunchKernelGGL(ms_block_radix_kernel<kRankLanes>, dim3(btiles), dim3(1024), 0, s, in, d0, n, mode, m0,
-                           smp0);
+        hipLaunchKernelGGL(ms_block_radix_kernel<kRankLanes>, dim3(btiles), dim3(1024), 0, s, in, d0, vin, v0, n,
+                           mode, m0, smp0);
+    else if (radix_kv)
+        hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, kMsItems, true, kBsThreads>), dim3(btiles),
+                           dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode, m0, smp0);
     else if (big && vin)
         hipLaunchKernelGGL((ms_block_sort_kernel<true, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s, in,
                            d0, vin, v0, n, mode, m0, smp0);

@@ -264,6 +264,10 @@ def test_merge_sort_radix_block_sort(gpu, block_sort, block, dtype):
                 assert torch.equal(sort(ku, algo="merge").cpu().view(torch.int32).long() & 0xFFFFFFFF, ref), n
             else:
                 assert torch.equal(sort(k, algo="merge").cpu(), torch.sort(k.cpu()).values), n
+                v = torch.arange(n, device="cuda", dtype=torch.int32)  # key-value: 8192-key radix tiles, stable
+                ks, vs = sort(k, values=v, algo="merge")
+                rk, ri = torch.sort(k.cpu().long(), stable=True)
+                assert torch.equal(ks.cpu().long(), rk) and torch.equal(vs.cpu().long(), ri), n
 
 
 @pytest.mark.gpu
