@@ -104,8 +104,9 @@ def _merge(keys: torch.Tensor, values: torch.Tensor | None):
     length; from 8M keys each pass first finds every tile's merge-path split
     in one launch (tuning knob merge_part), below that each merge block
     searches its own; key transforms fused into the first and last kernels.
-    Tuning knob merge_way=4 merges four runs per pass instead (built and
-    measured slower on MI355X: profiles/sort_r6.md)."""
+    Keys-only and key-value tiles are block-sorted by an LDS radix sort
+    (tuning knob merge_block_sort). A 4-way pass schedule lives in the tuning
+    library (cme_merge_sort4_tune; measured slower: profiles/sort_r6.md)."""
     if keys.dtype not in _MODES:
         raise TypeError(f"unsupported key dtype {keys.dtype}")
     k = keys.contiguous()

@@ -98,7 +98,7 @@ const TuneEntry kTuneTable[cme::kTuneCount] = {
     {"CME_SPMV_STREAM_ROWS", 0},
     {"CME_TILE_RES_MINR", 1},    {"CME_SPMV_SHORT_RPT", 1},     {"CME_MERGE_PART", -1},
     {"CME_MERGE_TILE", 4096},    {"CME_MERGE_BLOCK", 0},        {"CME_MERGE_SAMPLES", 1},
-    {"CME_MERGE_WAY", 2},        {"CME_MERGE_BLOCK_SORT", 1},
+    {"CME_MERGE_BLOCK_SORT", 1},
 };
 std::atomic<long> g_tune_val[cme::kTuneCount];
 std::atomic<int> g_tune_state[cme::kTuneCount];  // 0 not loaded, 1 from env / default, 2 set

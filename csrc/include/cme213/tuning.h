@@ -45,7 +45,6 @@ enum TuneKey : int {
     kTuneMergeTile,        // CME_MERGE_TILE: merge sort output tile per merge-pass block, 4096 or 8192 keys (8192 with partitions)
     kTuneMergeBlock,       // CME_MERGE_BLOCK: merge sort block-sort tile, 8192 (512 lanes) or 16384 keys (1024 lanes); 0 auto (16384 for keys only from 4M)
     kTuneMergeSamples,     // CME_MERGE_SAMPLES: merge sort run samples narrowing each partition search (1 on, 0 off)
-    kTuneMergeWay,         // CME_MERGE_WAY: merge sort passes with partition launches: 4-way (4) or 2-way (2)
     kTuneMergeBlockSort,   // CME_MERGE_BLOCK_SORT: keys-only 16384-key block sort, 1 LDS radix (4 digit passes), 0 merge network
     kTuneCount
 };

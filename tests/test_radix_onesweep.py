@@ -198,19 +198,35 @@ def test_merge_sort_partition_arms(gpu, part, tile, samples):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("way,part,samples,block", [(4, 8, 1, 0), (4, 8, 0, 8192), (4, 64, 1, 16384), (4, 4, 1, 8192),
-                                                    (2, 8, 1, 0)])
-def test_merge_sort_four_way_passes(gpu, way, part, samples, block):
-    """4-way merge passes (tuning knob merge_way; csrc/hip/sort.hip
+@pytest.mark.parametrize("part,samples,block", [(8, 1, 0), (8, 0, 8192), (64, 1, 16384), (4, 1, 8192)])
+def test_merge_sort_four_way_passes(gpu, tune_lib, part, samples, block):
+    """4-way merge passes (csrc/hip_tune/sort_tune.hip
     ms_partition4_kernel + ms_merge4_pass_kernel) sort keys and key-value
     pairs stably: groups of four runs, three (D empty), two and one at the
     array's end, an odd number of doublings (a last 2-way pass), ties across
-    every run boundary, and all-equal / presorted / reversed inputs."""
+    every run boundary, and all-equal / presorted / reversed inputs. The
+    4-way schedule is a tuning-library arm (cme_merge_sort4_tune)."""
+    from cme213x import _ext
     from cme213x.utils import tuning
+
+    _ext.proto(_ext.TUNE_PROTOS, "cme_merge_sort4_tune", "ppppppqipp")
+    modes = {torch.uint32: 0, torch.int32: 1, torch.float32: 2}
+
+    def sort(k, values=None, algo="merge"):  # the 4-way arm with ops.sort's calling convention
+        k = k.contiguous()
+        out, tmp = torch.empty_like(k), torch.empty_like(k)
+        vp = vo = vt = None
+        if values is not None:
+            vout, vtmp = torch.empty_like(values), torch.empty_like(values)
+            vp, vo, vt = values.data_ptr(), vout.data_ptr(), vtmp.data_ptr()
+        ws = torch.empty((k.numel() + 4095) // 4096 * 48 + 256, dtype=torch.uint8, device=k.device)
+        _ext.call_hip("cme_merge_sort4_tune", k.data_ptr(), out.data_ptr(), tmp.data_ptr(), vp, vo, vt, k.numel(),
+                      modes[k.dtype], ws.data_ptr(), _ext.stream_ptr(k.device))
+        return (out, vout) if values is not None else out
 
     g = torch.Generator(device="cuda").manual_seed(21)
     sizes = (8193, 3 * 8192 + 5, 5 * 8192, 16 * 8192 + 4095, 17 * 16384 + 1, 3 * (1 << 20) + 77, 9 * (1 << 20) + 5)
-    with tuning.override(merge_way=way, merge_part=part, merge_samples=samples, merge_block=block):
+    with tuning.override(merge_part=part, merge_samples=samples, merge_block=block):
         for n in sizes:
             k = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), device="cuda", dtype=torch.int32, generator=g)
             k[n // 2:] = k[n // 2:] % 13  # long runs of equal keys
