@@ -664,7 +664,18 @@ __global__ __launch_bounds__(256) void reduce_partial_kernel(const T* __restrict
     __shared__ T lds[4];
     T acc = Op::template identity<T>();
     const long long stride = (long long)gridDim.x * 256 * 4;
-    for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+    // four 16-B loads in flight per lane: 2^26 f32 cold 0.0497 -> 0.0452 ms
+    // (hip_tune/scan_tune.hip cme_reduce_tune, profiles/scan_r5.md round 6)
+    constexpr int U = 4;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        Vec4<T> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = load_v4(in, i + u * stride, n, Op::template identity<T>());
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = op(acc, op(op(v[u].x, v[u].y), op(v[u].z, v[u].w)));
+    }
+    for (; i < n; i += stride) {
         Vec4<T> v = load_v4(in, i, n, Op::template identity<T>());
         acc = op(acc, op(op(v.x, v.y), op(v.z, v.w)));
     }

@@ -197,3 +197,72 @@ CME_EXPORT int cme_scan_tree_tune(const float* in, float* out, long long n, int 
     hipLaunchKernelGGL((tile_tree_scan_kernel<float, true, 0>), dim3(g3), dim3(256), 0, s, in, out, n, nt, part);
     CME_LAUNCH_STATUS();
 }
+
+// ---------------------------------------------------------------------------
+// Tuning arms of the f32 sum reduction (production: scan.hip cme_reduce,
+// reduce_partial_kernel + reduce_final_kernel; BASELINE config #3).
+// benchmarks/tune_reduce.py times them cold.
+//   arm 0 production (grid 1024, one 16-B load in flight per lane)
+//   arm 1 four 16-B loads in flight per lane (grid 1024)
+//   arm 2 = 1 with grid 2048
+//   arm 3 = 1 with the final reduction by the last block to finish (one
+//         device-scope arrival atomic per block; no second launch)
+// part: >= 2048 floats, then a 256-B aligned counter word (arm 3: zero at
+// the first call, left zeroed).
+extern "C" int cme_reduce(const void* in, long long n, int dtype, int op, int algo, void* part, void* out,
+                          void* stream);  // production (libcme213_hip.so)
+namespace {
+template <int U, bool LAST>
+__global__ __launch_bounds__(256) void reduce_unr_kernel(const float* __restrict__ in, long long n,
+                                                         float* __restrict__ part, unsigned* __restrict__ counter,
+                                                         float* __restrict__ out) {
+    __shared__ float lds[4];
+    __shared__ unsigned s_last;
+    float acc = 0.f;
+    const long long stride = (long long)gridDim.x * 256 * 4;
+    long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        Vec4<float> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = load_v4(in, i + u * stride, n, 0.f);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = acc + ((v[u].x + v[u].y) + (v[u].z + v[u].w));
+    }
+    for (; i < n; i += stride) {
+        const Vec4<float> v = load_v4(in, i, n, 0.f);
+        acc = acc + ((v.x + v.y) + (v.z + v.w));
+    }
+    const float r = block_reduce<4>(acc, lds, OpAdd());
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+    if constexpr (LAST) {
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) s_last = atomicAdd(counter, 1u) == gridDim.x - 1u ? 1u : 0u;
+        lds_bcast_sync();
+        if (!s_last) return;
+        __threadfence();
+        float a = 0.f;
+        for (int j = threadIdx.x; j < (int)gridDim.x; j += 256) a = a + part[j];
+        const float t = block_reduce<4>(a, lds, OpAdd());
+        if (threadIdx.x == 0) {
+            *out = t;
+            *counter = 0u;
+        }
+    }
+}
+}  // namespace
+
+CME_EXPORT int cme_reduce_tune(const float* in, long long n, int arm, float* part, float* out, void* stream) {
+    hipStream_t s = as_stream(stream);
+    if (arm == 0) return cme_reduce(in, n, 0, 0, 0, part, out, stream);
+    unsigned* counter = (unsigned*)((char*)part + 2048 * 4);
+    const int grid = arm == 2 ? 2048 : 1024;
+    if (arm == 3) {
+        hipLaunchKernelGGL((reduce_unr_kernel<4, true>), dim3(grid), dim3(256), 0, s, in, n, part, counter, out);
+    } else {
+        hipLaunchKernelGGL((reduce_unr_kernel<4, false>), dim3(grid), dim3(256), 0, s, in, n, part, counter, out);
+        hipLaunchKernelGGL((reduce_final_kernel<float, OpAdd>), dim3(1), dim3(1024), 0, s, (const float*)part, grid,
+                           out, OpAdd());
+    }
+    CME_LAUNCH_STATUS();
+}
