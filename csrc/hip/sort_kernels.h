@@ -4,6 +4,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "cme213/common.h"
 #include "cme213/tuning.h"
@@ -559,10 +560,24 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
             smp.last[g] = sk[lp(e - 1)];
         }
     }
-    for (int i = t; i < cnt; i += NT) {
-        ko[base + i] = ms_key_out(sk[lp(i)], mode);
-        if constexpr (HAS_VALUES) vo[base + i] = sv[lp(i)];
-    }
+    // coalesced stores, unrolled: lane t writes t + q*NT (LDS word lp(t) +
+    // q*(NT + NT/16), immediate offsets), the key transform a compile-time
+    // branch (the dynamic loop with a run-time transform cost ~12 VALU per key)
+    auto out = [&](auto md) {
+        constexpr int MD = decltype(md)::value;
+        const int lt = lp(t);
+#pragma unroll
+        for (int q = 0; q < kMsItems; ++q) {
+            const int i = t + q * NT;
+            if (i < cnt) {
+                ko[base + i] = ms_key_out(sk[lt + q * (NT + NT / 16)], MD);
+                if constexpr (HAS_VALUES) vo[base + i] = sv[lt + q * (NT + NT / 16)];
+            }
+        }
+    };
+    if (mode == 0) out(std::integral_constant<int, 0>());
+    else if (mode == 1) out(std::integral_constant<int, 1>());
+    else out(std::integral_constant<int, 2>());
 }
 
 template <bool HAS_VALUES, int BS = kBsThreads>
@@ -735,10 +750,20 @@ __global__ __launch_bounds__(NT, NT == 1024 ? (ITEMS == 16 ? 8 : 4) : 4) void ms
             smp.last[base / smp.st + q] = s_keys[e - 1];
         }
     }
-    for (int i = tid; i < cnt; i += NT) {
-        ko[base + i] = ms_key_out(s_keys[i], mode_out);
-        if constexpr (HAS_VALUES) vo[base + i] = s_vals[i];
-    }
+    auto out = [&](auto md) {  // unrolled coalesced stores, compile-time key transform
+        constexpr int MD = decltype(md)::value;
+#pragma unroll
+        for (int q = 0; q < ITEMS; ++q) {
+            const int i = tid + q * NT;
+            if (i < cnt) {
+                ko[base + i] = ms_key_out(s_keys[i], MD);
+                if constexpr (HAS_VALUES) vo[base + i] = s_vals[i];
+            }
+        }
+    };
+    if (mode_out == 0) out(std::integral_constant<int, 0>());
+    else if (mode_out == 1) out(std::integral_constant<int, 1>());
+    else out(std::integral_constant<int, 2>());
 }
 
 // Cooperative merge-path search: the 128 lanes of `part` (waves 2*part and
@@ -906,11 +931,27 @@ __global__ __launch_bounds__(NT) void ms_merge_pass_kernel(const uint32_t* __res
     const long long j0 = (o0 - a0) - i0, j1 = (o1 - a0) - i1;
     int na = (int)(i1 - i0), nb = (int)(j1 - j0);
     if (na < 0 || nb < 0 || na + nb > TILE || i1 > la || j1 > lb) na = nb = 0;  // never out of range
-    for (int x = t; x < na + nb; x += NT) {
-        const bool ia = x < na;
-        const long long g = ia ? a0 + i0 + x : a0 + la + j0 + (x - na);
-        sk[lp(x)] = ki[g];
-        if constexpr (HAS_VALUES) sv[lp(x)] = vi[g];
+    {  // coalesced loads, unrolled (immediate LDS offsets): A's piece, then B's
+        const uint32_t* pa = ki + a0 + i0;
+        const uint32_t* pb = ki + a0 + la + j0 - na;  // B's x-th output slot reads pb[x]
+        const int lt = lp(t), c = na + nb;
+        if (c > 0) {  // block-uniform; all 16 loads in flight (clamped indices), then the LDS writes
+            uint32_t kk[kMsItems], vv[HAS_VALUES ? kMsItems : 1];
+#pragma unroll
+            for (int q = 0; q < kMsItems; ++q) {
+                const int x = min(t + q * NT, c - 1);
+                const uint32_t* src = x < na ? pa : pb;
+                kk[q] = src[x];
+                if constexpr (HAS_VALUES) vv[q] = vi[src - ki + x];
+            }
+#pragma unroll
+            for (int q = 0; q < kMsItems; ++q) {
+                if (t + q * NT < c) {
+                    sk[lt + q * (NT + NT / 16)] = kk[q];
+                    if constexpr (HAS_VALUES) sv[lt + q * (NT + NT / 16)] = vv[q];
+                }
+            }
+        }
     }
     __syncthreads();
     const int cnt = na + nb;
