@@ -565,6 +565,22 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
     // branch (the dynamic loop with a run-time transform cost ~12 VALU per key)
     auto out = [&](auto md) {
         constexpr int MD = decltype(md)::value;
+        if (cnt == NT * kMsItems && (base & 3) == 0) {
+            // a full tile: four consecutive keys per lane and store, 16 B
+            // (lane t takes keys 4(t + q NT) .. +3: one 16-key LDS group, so
+            // four contiguous padded words), a quarter of the store instructions
+#pragma unroll
+            for (int q = 0; q < kMsItems / 4; ++q) {
+                const int i = 4 * (t + q * NT);
+                const int w = lp(i);
+                uint4 o{ms_key_out(sk[w], MD), ms_key_out(sk[w + 1], MD), ms_key_out(sk[w + 2], MD),
+                        ms_key_out(sk[w + 3], MD)};
+                *reinterpret_cast<uint4*>(ko + base + i) = o;
+                if constexpr (HAS_VALUES)
+                    *reinterpret_cast<uint4*>(vo + base + i) = uint4{sv[w], sv[w + 1], sv[w + 2], sv[w + 3]};
+            }
+            return;
+        }
         const int lt = lp(t);
 #pragma unroll
         for (int q = 0; q < kMsItems; ++q) {
