@@ -1038,7 +1038,10 @@ int ms_sort_host(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_
         const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
         radix_block = cme_radix_lane_order(capturing ? 0 : 1) != 0;
     }
-    const bool huge = radix_block && !vin && mb == 32768;
+    // 32768-key radix tiles: asked for, or by size (one merge pass fewer pays
+    // from 6M to 24M keys: 8M 0.249 -> 0.233 ms, 16M 0.389 -> 0.374; 4M and
+    // 48M lose 2 %, raw_r6/merge_knobs_ab_r6.jsonl)
+    const bool huge = radix_block && !vin && (mb == 32768 || (mb == 0 && n >= (6ll << 20) && n <= (24ll << 20)));
     const bool big = huge || mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
     // key-value pairs: the radix block sort at 8192-key tiles (512 lanes)
     const bool radix_kv = radix_block && vin && !big;
