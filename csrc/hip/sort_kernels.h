@@ -674,7 +674,7 @@ __global__ __launch_bounds__(BS) void ms_block_sort_kernel(const uint32_t* __res
 // keys + 16 KiB of counts = 80 KiB and <= 64 VGPRs (8 waves per SIMD): two
 // blocks per CU.
 template <int RANK, int ITEMS = kMsItems, bool HAS_VALUES = false, int NT = 1024>
-__global__ __launch_bounds__(NT, NT == 1024 ? (ITEMS == 16 ? 8 : 4) : 4) void ms_block_radix_kernel(
+__global__ __launch_bounds__(NT, NT == 1024 && ITEMS == 16 && !HAS_VALUES ? 8 : 4) void ms_block_radix_kernel(
     const uint32_t* __restrict__ ki, uint32_t* __restrict__ ko, const uint32_t* __restrict__ vi,
     uint32_t* __restrict__ vo, long long n, int mode_in, int mode_out, MsSamples smp) {
     constexpr int NW = NT / kWave, TILE = NT * ITEMS;
@@ -1042,9 +1042,15 @@ int ms_sort_host(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_
     // from 6M to 24M keys: 8M 0.249 -> 0.233 ms, 16M 0.389 -> 0.374; 4M and
     // 48M lose 2 %, raw_r6/merge_knobs_ab_r6.jsonl)
     const bool huge = radix_block && !vin && (mb == 32768 || (mb == 0 && n >= (6ll << 20) && n <= (24ll << 20)));
-    const bool big = huge || mb == 16384 || (mb == 0 && !vin && n >= (4ll << 20));
+    // (key-value pairs through the radix block sort: 16384-key tiles from 4M
+    // too, 48M 2.49 -> 2.40 ms, 16M 0.705 -> 0.675, 4M 0.202 -> 0.190,
+    // raw_r6/merge_kv_block_ab_r6.jsonl)
+    const bool big = huge || mb == 16384 || (mb == 0 && (!vin || radix_block) && n >= (4ll << 20));
     // key-value pairs: the radix block sort at 8192-key tiles (512 lanes)
     const bool radix_kv = radix_block && vin && !big;
+    // key-value 16384-key radix tiles (merge_block=16384: 144 KiB LDS, one
+    // block per CU, one merge pass fewer)
+    const bool radix_kv_big = radix_block && vin && big;
     radix_block = radix_block && !vin && big;
     const long long btile = huge ? 4 * kBsTile : (big ? 2 * kBsTile : kBsTile);
     // partitions: tuning knob merge_part (G lanes per tile, 0 = in-block
@@ -1095,6 +1101,9 @@ int ms_sort_host(const uint32_t* in, uint32_t* out, uint32_t* tmp, const uint32_
     else if (radix_kv)
         hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, kMsItems, true, kBsThreads>), dim3(btiles),
                            dim3(kBsThreads), 0, s, in, d0, vin, v0, n, mode, m0, smp0);
+    else if (radix_kv_big)
+        hipLaunchKernelGGL((ms_block_radix_kernel<kRankLanes, kMsItems, true, 1024>), dim3(btiles), dim3(1024), 0, s,
+                           in, d0, vin, v0, n, mode, m0, smp0);
     else if (big && vin)
         hipLaunchKernelGGL((ms_block_sort_kernel<true, 2 * kBsThreads>), dim3(btiles), dim3(2 * kBsThreads), 0, s, in,
                            d0, vin, v0, n, mode, m0, smp0);
