@@ -565,7 +565,9 @@ __device__ __forceinline__ void ms_store_tile(uint32_t* sk, uint32_t* sv, const 
     // branch (the dynamic loop with a run-time transform cost ~12 VALU per key)
     auto out = [&](auto md) {
         constexpr int MD = decltype(md)::value;
-        if (cnt == NT * kMsItems && (base & 3) == 0) {
+        const bool al16 = ((reinterpret_cast<uintptr_t>(ko + base) |
+                            (HAS_VALUES ? reinterpret_cast<uintptr_t>(vo + base) : 0)) & 15) == 0;
+        if (cnt == NT * kMsItems && al16) {  // (the C API's in-place forms may hand in any 4-B aligned array)
             // a full tile: four consecutive keys per lane and store, 16 B
             // (lane t takes keys 4(t + q NT) .. +3: one 16-key LDS group, so
             // four contiguous padded words), a quarter of the store instructions

@@ -367,3 +367,31 @@ def test_radix_lane_ranks_low_entropy_stable(gpu, arm, kind):
     ref = torch.sort(k.long(), stable=True)
     assert torch.equal(ks.cpu().long(), ref.values)
     assert torch.equal(vs.cpu().long(), ref.indices)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("values", [False, True])
+def test_merge_sort_in_place_misaligned(gpu, values):
+    """The in-place C entry (cme_merge_sort_u32) on arrays that start 4 B past
+    a 16-B boundary: full output tiles must fall back from their 16-B stores
+    (csrc/hip/sort_kernels.h ms_store_tile) instead of faulting or tearing."""
+    from cme213x import _ext
+
+    n = 3 * (1 << 20) + 5
+    g = torch.Generator(device="cuda").manual_seed(41)
+    buf = torch.randint(0, 2**31 - 1, (n + 1,), device="cuda", dtype=torch.int32, generator=g)
+    keys = buf[1:]  # 4-B offset
+    orig = keys.cpu().long()
+    ref, ref_idx = torch.sort(orig, stable=True)
+    alt = torch.empty(n + 1, device="cuda", dtype=torch.int32)[1:]
+    vals = valt = None
+    if values:
+        vb = torch.arange(n + 1, device="cuda", dtype=torch.int32)
+        vals = vb[1:]
+        valt = torch.empty(n + 1, device="cuda", dtype=torch.int32)[1:]
+    _ext.call_hip("cme_merge_sort_u32", keys.data_ptr(), alt.data_ptr(), vals.data_ptr() if values else None,
+                  valt.data_ptr() if values else None, n, _ext.stream_ptr(gpu))
+    torch.cuda.synchronize(gpu)
+    assert torch.equal(keys.cpu().long(), ref)
+    if values:  # stable: each key carries its original position (values started at 1)
+        assert torch.equal(vals.cpu().long(), ref_idx + 1)
