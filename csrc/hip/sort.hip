@@ -50,7 +50,7 @@ CME_EXPORT long long cme_radix_ws_bytes(long long n) {
 // 0.821; 16M int32 key-value 0.378 vs 0.440). With the match gone the larger
 // tiles win (digit runs of ~32 keys: fewer partial lines written), where they
 // lost to the barrier rounds before.
-static int radix_ds_variant() { return (int)(cme::tune_get(cme::kTuneRadixDS) & 15); }
+static int radix_ds_variant() { return (int)(cme::tune_get(cme::kTuneRadixDS) & 31); }
 
 namespace {
 // Lane-order check for kRankLanes: one block; every wave runs `trials`
@@ -135,7 +135,12 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
     }
     const bool lanes = (dsv & 8) != 0;
     const bool wide = (dsv & 4) != 0;  // 8192-key downsweep tiles
-    const long long dtile = wide ? 2 * kSortTile : kSortTile;
+    // 16384-key tiles (bit 16: 1024 lanes, lane ranks only): digit runs of
+    // ~64 keys, but one block per CU (83 KiB LDS, 82 VGPRs); measured 16M
+    // 0.2195 -> 0.245-0.251 ms, 48M 0.679 -> 0.661 without prefetch
+    // (raw_r6/radix_ds16k_ab_r6.jsonl) -- an arm, not the default
+    const bool huge = lanes && (dsv & 16) != 0;
+    const long long dtile = huge ? 4 * kSortTile : (wide ? 2 * kSortTile : kSortTile);
     const long long tiles = (n + dtile - 1) / dtile;
     const int cap = radix_max_blocks();
     int nb = tiles < cap ? (int)tiles : cap;
@@ -172,7 +177,10 @@ CME_EXPORT int cme_radix_sort(const uint32_t* in, uint32_t* out, uint32_t* tmp, 
         hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins), dim3(1024), 0, s, counts, nb, totals);
 #define CME_DS(V, A, P)                                                                                           \
     do {                                                                                                          \
-        if (wide)                                                                                                 \
+        if (huge && A == kRankLanes)                                                                              \
+            hipLaunchKernelGGL((radix_downsweep_kernel<V, kRankLanes, P, 1024>), dim3(nb), dim3(1024), 0, s, ki, ko,  \
+                               vi, vo, n, chunk, shift, nb, counts, totals, mi, mo);                              \
+        else if (wide)                                                                                            \
             hipLaunchKernelGGL((radix_downsweep_kernel<V, A, P, 512>), dim3(nb), dim3(512), 0, s, ki, ko, vi, vo, n, \
                                chunk, shift, nb, counts, totals, mi, mo);                                         \
         else                                                                                                      \

@@ -22,7 +22,7 @@ enum TuneKey : int {
     kTuneDistGateSpins,    // CME_DIST_GATE_SPINS: polls of a fused border wait before it gives up
     kTuneDistFakeXchgUs,   // CME_DIST_FAKE_XCHG_US: rehearsal / test delay of each exchange
     kTuneRadixMaxBlocks,   // CME_RADIX_MAXBLOCKS: reduce-then-scan grid cap
-    kTuneRadixDS,          // CME_RADIX_DS: downsweep arm bits (1 group atomics, 2 prefetch, 4 8192-key tiles, 8 lane ranks)
+    kTuneRadixDS,          // CME_RADIX_DS: downsweep arm bits (1 group atomics, 2 prefetch, 4 8192-key tiles, 8 lane ranks, 16 16384-key tiles with lane ranks)
     kTuneStream2Chunk,     // CME_STREAM2_CHUNK
     kTuneStreamNChunk,     // CME_STREAMN_CHUNK
     kTuneStreamNRounds,    // CME_STREAMN_ROUNDS
